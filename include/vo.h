@@ -1,0 +1,229 @@
+/*
+ * vo.h — C-ABI of libvo, the MI355X-native stereo visual-odometry front end.
+ *
+ * Drop-in boundary.  The reference (ivario123/r7020e-visual-
+ * odometry, MATLAB) has no native interface: its per-frame path calls
+ * MathWorks toolbox functions from VO.m.  Each entry point below replaces one
+ * of those calls; a MATLAB maintainer binds them through the MEX gateways
+ * shown in INTEGRATION.md (path shadowing), a Python user through ctypes
+ * (r7020e-visual-odometry_amd/vo.py).
+ *
+ *   entry point            replaces (reference call site)
+ *   ---------------------  ---------------------------------------------------
+ *   vo_sift                detectSIFTFeatures + extractFeatures(...,"SIFT")
+ *                          VO.m:79-84
+ *   vo_match               matchFeatures(F1, F2)  VO.m:87,283,293,311,323
+ *   vo_track               find_remaining_points  VO.m:280-334 (4 matches +
+ *                          gathers), fused on device
+ *   vo_triangulate         triangulate(x1, x2, P1, P2)  VO.m:113-116,
+ *                          CreateLandmarksFromFeatures.m:7
+ *   vo_estworldpose        estworldpose(imagePts, worldPts, intrinsics)
+ *                          VO.m:123-127 (P3P + MSAC)
+ *   vo_landmarks           new-landmark filter VO.m:145-158 +
+ *                          CreateLandmarksFromFeatures.m:1-21
+ *   vo_step / vo_step_batch the whole loop body VO.m:70-161 (features stay
+ *                          device-resident between frames)
+ *   vo_sift_match_batch    VO.m:79-87 for a batch of independent stereo pairs
+ *                          (the benchmark workload, BASELINE.json configs[1])
+ *
+ * Conventions
+ *  - Return value: VO_OK (0) or a negative VO_ERR_* code.  vo_last_error()
+ *    gives a message.  VO_ERR_TOO_FEW_POINTS / VO_ERR_NO_CONSENSUS mirror the
+ *    errors estworldpose throws (the reference crashes; we report and the
+ *    step holds the previous pose).
+ *  - Buffers are caller-allocated host memory with explicit capacities, unless
+ *    a function name ends in _dev (device pointers, stream-ordered).
+ *  - Images: uint8, row-major with leading dimension `ld` (bytes per row).
+ *    (MATLAB is column-major: the MEX shim passes the transpose view, see
+ *    INTEGRATION.md.)
+ *  - Image coordinates are MATLAB 1-based pixel coordinates (x = column).
+ *  - Index pairs are 1-based uint32 [P][2] row-major, ascending in column 0,
+ *    exactly as matchFeatures returns them.
+ *  - Matrices are row-major doubles: P1/P2 3x4 premultiply camera matrices,
+ *    K 3x3, rigid transforms 4x4 (R2022b rigidtform3d.A convention).
+ *  - One context per device; a context is not thread-safe.
+ */
+#ifndef VO_H
+#define VO_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VO_OK                  0
+#define VO_ERR_ARG            -1
+#define VO_ERR_HIP            -2
+#define VO_ERR_TOO_FEW_POINTS -3
+#define VO_ERR_NO_CONSENSUS   -4
+#define VO_ERR_CAPACITY       -5
+#define VO_ERR_STATE          -6
+
+#define VO_DESC_LEN 128
+
+/* detectSIFTFeatures / extractFeatures defaults (MATLAB R2022b+).
+ * contrast_threshold is in OpenCV units: MATLAB's ContrastThreshold 0.0133
+ * equals 0.04 / NumLayersInOctave. */
+typedef struct {
+    int32_t n_octave_layers;      /* NumLayersInOctave, 3 */
+    float   sigma;                /* Sigma, 1.6 */
+    float   contrast_threshold;   /* 0.04  (= 0.0133 * 3) */
+    float   edge_threshold;       /* EdgeThreshold, 10 */
+    int32_t upsample;             /* 1: first octave is the x2 upsampled image */
+    int32_t max_keypoints;        /* capacity per image (keypoints beyond it are dropped, flagged) */
+} vo_sift_params;
+
+/* matchFeatures defaults: Method Exhaustive, Metric SSD, MatchThreshold 1.0
+ * (percent), MaxRatio 0.6, Unique false. */
+typedef struct {
+    float match_threshold;        /* percent; SSD threshold = 0.04 * match_threshold on unit vectors */
+    float max_ratio;              /* 0.6 */
+} vo_match_params;
+
+/* estworldpose defaults + the BASELINE config (2048 hypotheses). */
+typedef struct {
+    int32_t  max_num_trials;      /* 2048 */
+    double   confidence;          /* percent, 99 */
+    double   max_reprojection_error; /* pixels, 1 */
+    uint32_t seed;                /* Philox key (frame index is mixed in by vo_step) */
+} vo_ransac_params;
+
+typedef struct {
+    double P1[12];   /* left camera 3x4 (VO.m:27-29) */
+    double P2[12];   /* right camera 3x4 (VO.m:30-32) */
+    double K[9];     /* left intrinsics (VO.m:35-38,50) */
+} vo_calib;
+
+typedef struct {
+    float   x, y;        /* Location, 1-based */
+    float   size;        /* keypoint diameter in image pixels (OpenCV KeyPoint.size) */
+    float   angle;       /* orientation in degrees [0,360) (OpenCV convention) */
+    float   response;    /* |DoG| at the refined extremum (Metric) */
+    int32_t octave;      /* octave index, -1 = upsampled */
+    int32_t layer;       /* layer within octave 1..n_octave_layers */
+    float   scale;       /* Scale = size / 2 in image pixels */
+} vo_keypoint;
+
+typedef struct vo_ctx vo_ctx;
+
+/* Defaults for every parameter block. */
+void vo_default_sift_params(vo_sift_params* p);
+void vo_default_match_params(vo_match_params* p);
+void vo_default_ransac_params(vo_ransac_params* p);
+
+/* Create a context on HIP device `device` for images of rows x cols, able to
+ * process up to max_batch stereo frames per call.  calib may be NULL (then
+ * vo_step/vo_landmarks are unavailable until vo_set_calib). Returns NULL on
+ * failure (message via vo_last_error(NULL)). */
+vo_ctx* vo_create(int device, int rows, int cols, int max_batch,
+                  const vo_calib* calib, const vo_sift_params* sift,
+                  const vo_match_params* match, const vo_ransac_params* ransac);
+void vo_destroy(vo_ctx* ctx);
+int  vo_set_calib(vo_ctx* ctx, const vo_calib* calib);
+const char* vo_last_error(const vo_ctx* ctx);
+
+/* detectSIFTFeatures + extractFeatures for one image (host buffers).
+ * kps[capacity], desc[capacity][128] (uint8 values; MATLAB gets them as
+ * single).  *n_out = number of keypoints (may exceed capacity: then only
+ * `capacity` are written and VO_ERR_CAPACITY is returned). */
+int vo_sift(vo_ctx* ctx, const uint8_t* img, int rows, int cols, int ld,
+            vo_keypoint* kps, uint8_t* desc, int capacity, int* n_out);
+
+/* matchFeatures(F1, F2) on SIFT descriptors (uint8 rows of 128).
+ * pairs[capacity][2] 1-based; *n_pairs = matches found. */
+int vo_match(vo_ctx* ctx, const uint8_t* F1, int n1, const uint8_t* F2, int n2,
+             uint32_t* pairs, int capacity, int* n_pairs);
+
+/* find_remaining_points (VO.m:280-334) on device.  old = previous frame's
+ * stereo-aligned set (n_old rows, left/right row-aligned); cur = current
+ * frame's full left (n_cl) / right (n_cr) sets.  Writes K row-aligned rows:
+ * idx_out[K][3] = 1-based rows {old_row, cur_left_row, cur_right_row}
+ * (old left and right stay row-aligned through VO.m:287-329), *K_out. */
+int vo_track(vo_ctx* ctx,
+             const uint8_t* old_l_desc, const uint8_t* old_r_desc, int n_old,
+             const uint8_t* cur_l_desc, int n_cl, const uint8_t* cur_r_desc, int n_cr,
+             uint32_t* idx_out, int capacity, int* K_out);
+
+/* triangulate: n points, x1/x2 [n][2] float (1-based pixels), P1/P2 3x4
+ * row-major -> X [n][3] double (values rounded through single, as MATLAB
+ * returns single for single inputs). */
+int vo_triangulate(vo_ctx* ctx, const float* x1, const float* x2, int n,
+                   const double P1[12], const double P2[12], double* X);
+
+/* estworldpose: img [n][2] double (1-based pixels), world [n][3] double,
+ * K 3x3 -> T 4x4 camera pose in world (rigidtform3d.A), inliers[n] (0/1),
+ * *n_inliers.  frame_key is mixed into the Philox key.  Returns
+ * VO_ERR_TOO_FEW_POINTS (n < 4) or VO_ERR_NO_CONSENSUS like MATLAB throws. */
+int vo_estworldpose(vo_ctx* ctx, const double* img, const double* world, int n,
+                    const double K[9], const vo_ransac_params* params, uint32_t frame_key,
+                    double T[16], uint8_t* inliers, int* n_inliers);
+
+/* new-landmark filter (VO.m:145-158) + CreateLandmarksFromFeatures.
+ * l_pos/r_pos [S][2] current stereo-matched locations; old_l/old_r [K][2]
+ * remaining_old_features locations; pose 4x4 world pose.  Appends rows to
+ * out[capacity][3]; *rows_out = rows appended (max(2, last kept odd index),
+ * zero rows kept exactly as the reference does). */
+int vo_landmarks(vo_ctx* ctx, const float* l_pos, const float* r_pos, int S,
+                 const float* old_l, const float* old_r, int K,
+                 const double pose[16], double* out, int capacity, int* rows_out);
+
+/* ---- fused per-frame step (the VO.m loop body) ----------------------- */
+typedef struct {
+    int32_t status;          /* VO_OK, or VO_ERR_* for this frame (pose held) */
+    int32_t n_left, n_right; /* detected keypoints */
+    int32_t n_stereo;        /* stereo matches S (VO.m:87) */
+    int32_t n_tracked;       /* K after find_remaining_points (0 on frame 1) */
+    int32_t n_inliers;       /* MSAC inliers */
+    int32_t n_landmarks;     /* landmark rows appended this frame */
+    int32_t pad;
+    double  rel_pose[16];    /* rel_pose.A (identity on frame 1) */
+    double  pose[16];        /* world pose after this frame (pose.A) */
+} vo_step_out;
+
+/* Process one stereo frame.  Keeps `features` (stereo subset) on device for
+ * the next call.  Landmarks accumulate inside the context (vo_get_landmarks). */
+int vo_step(vo_ctx* ctx, const uint8_t* left, const uint8_t* right, int ld, vo_step_out* out);
+
+/* Process B consecutive frames (host buffers, B*rows*ld bytes each).  The
+ * per-frame work is batched across frames on the GPU; only the 4x4 pose
+ * chain is sequential (host).  Equivalent to B calls of vo_step. */
+int vo_step_batch(vo_ctx* ctx, const uint8_t* lefts, const uint8_t* rights, int ld, int B,
+                  vo_step_out* outs);
+/* Same, inputs already in device memory (tightly packed rows*cols each). */
+int vo_step_batch_dev(vo_ctx* ctx, const uint8_t* d_lefts, const uint8_t* d_rights, int B,
+                      vo_step_out* outs);
+
+/* Landmarks accumulated so far ([rows][3] double, world frame). */
+int vo_get_landmarks(vo_ctx* ctx, double* out, int capacity, int* rows);
+/* Reset loop state (features, pose, landmarks). */
+int vo_reset(vo_ctx* ctx);
+
+/* ---- benchmark workload: SIFT + stereo match on B independent pairs ---- */
+typedef struct {
+    int32_t n_left, n_right, n_stereo, flags;
+} vo_pair_stats;
+
+/* Device buffers: d_lefts/d_rights are B tightly packed rows*cols images.
+ * Stream-ordered on the context's stream; stats (host) are written after the
+ * call completes (the call synchronises only when stats != NULL). */
+int vo_sift_match_batch_dev(vo_ctx* ctx, const uint8_t* d_lefts, const uint8_t* d_rights, int B,
+                            vo_pair_stats* stats);
+
+/* Device-side results of the last batched call, for parity tests:
+ * keypoints and descriptors of image i (2*frame + side) and stereo pairs of
+ * a frame.  Host output buffers. */
+int vo_fetch_keypoints(vo_ctx* ctx, int image, vo_keypoint* kps, uint8_t* desc, int capacity, int* n);
+int vo_fetch_stereo_pairs(vo_ctx* ctx, int frame, uint32_t* pairs, int capacity, int* n);
+
+/* HIP stream the context launches on (hipStream_t as void*), and per-kernel
+ * timing over the last call (for bench.py's roofline; ms). */
+void* vo_stream(vo_ctx* ctx);
+int vo_set_profiling(vo_ctx* ctx, int enable);
+int vo_kernel_times(vo_ctx* ctx, const char** names, double* ms, int* calls, int capacity, int* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VO_H */
