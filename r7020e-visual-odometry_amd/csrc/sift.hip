@@ -1,0 +1,744 @@
+// sift.hip — detectSIFTFeatures + extractFeatures (VO.m:79-84) on gfx950.
+//
+// Pipeline per batch of n_img images:
+//   k_base_h / k_blur_h   horizontal Gaussian pass, row tile staged in LDS
+//                         (octave 0 computes the x2 upsample on the fly)
+//   k_blur_v              vertical pass from an LDS column tile; writes G_i and
+//                         the DoG D_{i-1} = G_i - G_{i-1} in the same pass
+//   k_down                next octave base = G[o-1][L](2y, 2x)
+//   k_ext_mask            26-neighbour extremum test, one wave per 64 columns,
+//                         ballot -> 64-bit mask per word
+//   k_scan_words/k_emit   deterministic compaction in (octave, layer, row, col)
+//                         scan order (prefix sum, no atomic append)
+//   k_refine_orient       one wave per candidate: Newton refinement (wave-
+//                         uniform), orientation histogram (lanes stride the
+//                         window, 2^-20 fixed-point LDS atomics), peaks by ballot
+//   k_scan_cands/k_expand keypoint list in candidate order, then peak order
+//   k_desc                one wave per keypoint: 4x4x8 trilinear histogram
+//                         (fixed-point LDS atomics), norms as a wave tree
+// Every float expression follows oracle/sift_ref.c operation for operation.
+#include "vo_internal.h"
+#include <cstring>
+#include <cmath>
+
+namespace vo {
+
+struct Kern { float k[VO_SIFT_MAX_RADIUS + 1]; int r; };
+
+// ---------------------------------------------------------------------------
+// geometry (host)
+// ---------------------------------------------------------------------------
+void build_pyramid_geometry(Pyramid& py, int rows, int cols, int n_img, const vo_sift_params& p)
+{
+    memset(&py, 0, sizeof(py));
+    const int L = p.n_octave_layers;
+    py.L = L;
+    py.n_img = n_img;
+    py.n_oct = vo_num_octaves(rows, cols, p.upsample);
+    int R = p.upsample ? rows * 2 : rows, C = p.upsample ? cols * 2 : cols;
+    size_t off = 0;
+    size_t tmp_plane = 0;
+    for (int o = 0; o < py.n_oct; ++o) {
+        OctGeom& g = py.oct[o];
+        if (o) { R /= 2; C /= 2; }
+        g.rows = R; g.cols = C;
+        g.pitch = (C + 63) / 64 * 64;
+        g.plane = (size_t)g.rows * g.pitch;
+        for (int i = 0; i < L + 3; ++i) { g.g_off[i] = off; off += g.plane * n_img; }
+        for (int i = 0; i < L + 2; ++i) { g.d_off[i] = off; off += g.plane * n_img; }
+        if (g.plane > tmp_plane) tmp_plane = g.plane;
+    }
+    py.total = off;
+    py.tmp_plane = tmp_plane;
+    double sig[VO_SIFT_MAX_LAYERS];
+    vo_level_sigmas(L, p.sigma, sig);
+    py.krad[0] = vo_gauss_kernel(vo_base_sigma(p.sigma, p.upsample), py.kern[0], VO_SIFT_MAX_RADIUS + 1);
+    for (int i = 1; i < L + 3; ++i) py.krad[i] = vo_gauss_kernel(sig[i], py.kern[i], VO_SIFT_MAX_RADIUS + 1);
+    int w = 0, b = 0;
+    for (int o = 0; o < py.n_oct; ++o) {
+        int ir = py.oct[o].rows - 2 * VO_SIFT_BORDER, ic = py.oct[o].cols - 2 * VO_SIFT_BORDER;
+        if (ir < 0) ir = 0;
+        if (ic < 0) ic = 0;
+        py.wrow[o] = (ic + 63) / 64;
+        for (int l = 0; l < L; ++l) { py.wbase[b++] = w; w += ir * py.wrow[o]; }
+    }
+    py.wbase[b] = w;
+    py.n_words = w;
+}
+
+hipError_t sift_alloc(SiftBuffers& b, const Pyramid& py, int kp_cap, int cand_cap)
+{
+    const int n = py.n_img;
+    b.n_img = n; b.kp_cap = kp_cap; b.cand_cap = cand_cap;
+    hipError_t e;
+#define VO_ALLOC(ptr, bytes) do { e = hipMalloc((void**)&(ptr), (bytes)); if (e != hipSuccess) return e; } while (0)
+    VO_ALLOC(b.arena, sizeof(float) * py.total);
+    VO_ALLOC(b.tmp, sizeof(float) * py.tmp_plane * n);
+    VO_ALLOC(b.mask, sizeof(unsigned long long) * (size_t)py.n_words * n + 8);
+    VO_ALLOC(b.woff, sizeof(uint32_t) * (size_t)py.n_words * n + 8);
+    VO_ALLOC(b.cand, sizeof(uint32_t) * (size_t)cand_cap * n);
+    VO_ALLOC(b.n_cand, sizeof(int) * n);
+    VO_ALLOC(b.cout, sizeof(CandOut) * (size_t)cand_cap * n);
+    VO_ALLOC(b.koff, sizeof(uint32_t) * (size_t)cand_cap * n);
+    VO_ALLOC(b.n_kp, sizeof(int) * n);
+    VO_ALLOC(b.kp, sizeof(vo_keypoint) * (size_t)kp_cap * n);
+    VO_ALLOC(b.kpi, sizeof(KpInt) * (size_t)kp_cap * n);
+    VO_ALLOC(b.desc, (size_t)VO_DESC_LEN * kp_cap * n);
+    VO_ALLOC(b.meta, sizeof(DescMeta) * (size_t)kp_cap * n);
+#undef VO_ALLOC
+    return hipSuccess;
+}
+
+void sift_free(SiftBuffers& b)
+{
+    hipFree(b.arena); hipFree(b.tmp); hipFree(b.mask); hipFree(b.woff); hipFree(b.cand); hipFree(b.n_cand);
+    hipFree(b.cout); hipFree(b.koff); hipFree(b.n_kp); hipFree(b.kp); hipFree(b.kpi); hipFree(b.desc); hipFree(b.meta);
+    b = SiftBuffers();
+}
+
+// ---------------------------------------------------------------------------
+// Gaussian pyramid
+// ---------------------------------------------------------------------------
+#define HB 256   // outputs per block of the horizontal pass
+
+__device__ __forceinline__ float up_sample(const uint8_t* __restrict__ img, int ld, int rows, int cols, int y, int x)
+{
+    int ya = y >> 1, yb = (y & 1) ? (ya + 1 < rows ? ya + 1 : rows - 1) : (ya > 0 ? ya - 1 : 0);
+    int xa = x >> 1, xb = (x & 1) ? (xa + 1 < cols ? xa + 1 : cols - 1) : (xa > 0 ? xa - 1 : 0);
+    float ha = 0.75f * (float)img[ya * ld + xa] + 0.25f * (float)img[ya * ld + xb];
+    float hb = 0.75f * (float)img[yb * ld + xa] + 0.25f * (float)img[yb * ld + xb];
+    return 0.75f * ha + 0.25f * hb;
+}
+
+// octave-0 base: (upsample) + horizontal pass.  grid (ceil(C/HB), R, n_img)
+template <bool UP>
+__global__ __launch_bounds__(HB) void k_base_h(ImageSrc src, int rows, int cols, int R, int C, float* __restrict__ tmp,
+                                               size_t tmp_plane, int tpitch, Kern K)
+{
+    __shared__ float buf[HB + 2 * VO_SIFT_MAX_RADIUS];
+    const int img = blockIdx.z, y = blockIdx.y, x0 = blockIdx.x * HB, r = K.r;
+    const uint8_t* base = ((img & 1) ? src.right : src.left) + (size_t)(img >> 1) * src.frame_stride;
+    for (int t = threadIdx.x; t < HB + 2 * r; t += HB) {
+        int x = vo_reflect101(x0 - r + t, C);
+        buf[t] = UP ? up_sample(base, src.ld, rows, cols, y, x) : (float)base[y * src.ld + x];
+    }
+    __syncthreads();
+    int x = x0 + threadIdx.x;
+    if (x >= C) return;
+    const float* s = buf + threadIdx.x + r;
+    float acc = K.k[0] * s[0];
+    for (int j = 1; j <= r; ++j) acc = fmaf(K.k[j], s[-j] + s[j], acc);
+    tmp[img * tmp_plane + (size_t)y * tpitch + x] = acc;
+}
+
+// horizontal pass on a float plane.  grid (ceil(C/HB), R, n_img)
+__global__ __launch_bounds__(HB) void k_blur_h(const float* __restrict__ src, size_t plane, int pitch, int R, int C,
+                                               float* __restrict__ tmp, size_t tmp_plane, Kern K)
+{
+    __shared__ float buf[HB + 2 * VO_SIFT_MAX_RADIUS];
+    const int img = blockIdx.z, y = blockIdx.y, x0 = blockIdx.x * HB, r = K.r;
+    const float* row = src + img * plane + (size_t)y * pitch;
+    for (int t = threadIdx.x; t < HB + 2 * r; t += HB) buf[t] = row[vo_reflect101(x0 - r + t, C)];
+    __syncthreads();
+    int x = x0 + threadIdx.x;
+    if (x >= C) return;
+    const float* s = buf + threadIdx.x + r;
+    float acc = K.k[0] * s[0];
+    for (int j = 1; j <= r; ++j) acc = fmaf(K.k[j], s[-j] + s[j], acc);
+    tmp[img * tmp_plane + (size_t)y * pitch + x] = acc;
+}
+
+#define VT_W 64
+#define VT_H 32
+// vertical pass + DoG.  block (64,4), grid (ceil(C/64), ceil(R/32), n_img)
+template <bool DOG>
+__global__ __launch_bounds__(256) void k_blur_v(const float* __restrict__ tmp, size_t tmp_plane, int pitch, int R, int C,
+                                                float* __restrict__ g_out, const float* __restrict__ g_prev,
+                                                float* __restrict__ d_out, size_t plane, Kern K)
+{
+    __shared__ float tile[(VT_H + 2 * VO_SIFT_MAX_RADIUS) * VT_W];
+    const int img = blockIdx.z, x0 = blockIdx.x * VT_W, y0 = blockIdx.y * VT_H, r = K.r;
+    const int tx = threadIdx.x, ty = threadIdx.y;
+    const int x = x0 + tx;
+    const float* src = tmp + img * tmp_plane;
+    for (int rr = ty; rr < VT_H + 2 * r; rr += 4) {
+        int y = vo_reflect101(y0 - r + rr, R);
+        tile[rr * VT_W + tx] = x < C ? src[(size_t)y * pitch + x] : 0.0f;
+    }
+    __syncthreads();
+    if (x >= C) return;
+    for (int q = 0; q < VT_H / 4; ++q) {
+        int yl = ty + 4 * q, y = y0 + yl;
+        if (y >= R) break;
+        const float* s = tile + (yl + r) * VT_W + tx;
+        float acc = K.k[0] * s[0];
+        for (int j = 1; j <= r; ++j) acc = fmaf(K.k[j], s[-j * VT_W] + s[j * VT_W], acc);
+        size_t o = img * plane + (size_t)y * pitch + x;
+        g_out[o] = acc;
+        if (DOG) d_out[o] = acc - g_prev[o];
+    }
+}
+
+// next octave base.  grid over outputs
+__global__ void k_down(const float* __restrict__ src, size_t splane, int spitch, float* __restrict__ dst, size_t dplane,
+                       int dpitch, int R, int C, int n_img)
+{
+    size_t n = (size_t)n_img * R * C;
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n; t += (size_t)gridDim.x * blockDim.x) {
+        int img = (int)(t / ((size_t)R * C));
+        int rem = (int)(t - (size_t)img * R * C);
+        int y = rem / C, x = rem - y * C;
+        dst[img * dplane + (size_t)y * dpitch + x] = src[img * splane + (size_t)(2 * y) * spitch + 2 * x];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// extrema: masks, scan, emit
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void decode_word(const Pyramid* __restrict__ py, int w, int& o, int& layer, int& row, int& k)
+{
+    const int L = py->L;
+    int b = 0;
+    const int nb = py->n_oct * L;
+    while (b + 1 < nb && py->wbase[b + 1] <= w) ++b;
+    o = b / L;
+    layer = b - o * L + 1;
+    int rel = w - py->wbase[b];
+    int wr = py->wrow[o];
+    row = VO_SIFT_BORDER + rel / wr;
+    k = rel - (rel / wr) * wr;
+}
+
+// one wave per word.  block 256 (4 words), grid-stride
+__global__ __launch_bounds__(256) void k_ext_mask(const Pyramid* __restrict__ py, const float* __restrict__ arena,
+                                                  unsigned long long* __restrict__ mask, int n_img, float thr)
+{
+    const int lane = threadIdx.x & 63;
+    const int nw = py->n_words;
+    const long total = (long)nw * n_img;
+    for (long t = (long)blockIdx.x * 4 + (threadIdx.x >> 6); t < total; t += (long)gridDim.x * 4) {
+        const int img = (int)(t / nw), w = (int)(t - (long)img * nw);
+        int o, layer, r, k;
+        decode_word(py, w, o, layer, r, k);
+        const OctGeom& g = py->oct[o];
+        const int c = VO_SIFT_BORDER + 64 * k + lane;
+        bool ext = false;
+        if (c < g.cols - VO_SIFT_BORDER) {
+            const float* cur = arena + g.d_off[layer] + img * g.plane + (size_t)r * g.pitch + c;
+            const float* prv = arena + g.d_off[layer - 1] + img * g.plane + (size_t)r * g.pitch + c;
+            const float* nxt = arena + g.d_off[layer + 1] + img * g.plane + (size_t)r * g.pitch + c;
+            const float val = cur[0];
+            if (fabsf(val) > thr) {
+                ext = true;
+                const int P = g.pitch;
+                if (val > 0) {
+#pragma unroll
+                    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                        for (int dx = -1; dx <= 1; ++dx) {
+                            const int q = dy * P + dx;
+                            ext = ext && (val >= prv[q]) && (val >= nxt[q]) && (val >= cur[q]);
+                        }
+                } else {
+#pragma unroll
+                    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                        for (int dx = -1; dx <= 1; ++dx) {
+                            const int q = dy * P + dx;
+                            ext = ext && (val <= prv[q]) && (val <= nxt[q]) && (val <= cur[q]);
+                        }
+                }
+            }
+        }
+        unsigned long long b = __ballot(ext);
+        if (lane == 0) mask[t] = b;
+    }
+}
+
+// Block-wide exclusive scan of one value per thread (1024 threads).
+__device__ __forceinline__ uint32_t block_exscan_1024(uint32_t v, uint32_t* sh, uint32_t* total)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        uint32_t s = lane < 16 ? sh[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            uint32_t y = __shfl_up(s, o);
+            if (lane >= o) s += y;
+        }
+        if (lane < 16) sh[16 + lane] = s;
+    }
+    __syncthreads();
+    uint32_t before = wid ? sh[16 + wid - 1] : 0;
+    *total = sh[16 + 15];
+    __syncthreads();
+    return before + x - v;
+}
+
+// per image: exclusive scan of popcount(mask) -> woff, n_cand.  grid n_img, block 1024
+__global__ __launch_bounds__(1024) void k_scan_words(const unsigned long long* __restrict__ mask, uint32_t* __restrict__ woff,
+                                                     int* __restrict__ n_cand, int nw)
+{
+    __shared__ uint32_t sh[32];
+    const int img = blockIdx.x, tid = threadIdx.x;
+    const unsigned long long* m = mask + (size_t)img * nw;
+    uint32_t* wo = woff + (size_t)img * nw;
+    const int chunk = (nw + 1023) / 1024;
+    const int a = tid * chunk, e = min(a + chunk, nw);
+    uint32_t s = 0;
+    for (int w = a; w < e; ++w) s += (uint32_t)__popcll(m[w]);
+    uint32_t total;
+    uint32_t base = block_exscan_1024(s, sh, &total);
+    for (int w = a; w < e; ++w) { wo[w] = base; base += (uint32_t)__popcll(m[w]); }
+    if (tid == 0) n_cand[img] = (int)total;
+}
+
+__global__ void k_emit(const Pyramid* __restrict__ py, const unsigned long long* __restrict__ mask,
+                       const uint32_t* __restrict__ woff, uint32_t* __restrict__ cand, int cand_cap, int n_img)
+{
+    const int nw = py->n_words;
+    const long total = (long)nw * n_img;
+    for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+        unsigned long long m = mask[t];
+        if (!m) continue;
+        const int img = (int)(t / nw), w = (int)(t - (long)img * nw);
+        int o, layer, r, k;
+        decode_word(py, w, o, layer, r, k);
+        uint32_t idx = woff[t];
+        while (m) {
+            int bit = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            if (idx < (uint32_t)cand_cap) cand[(size_t)img * cand_cap + idx] = pack_cand(o, layer, r, VO_SIFT_BORDER + 64 * k + bit);
+            idx++;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// refinement + orientation: one wave (block of 64) per candidate
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool flat_item(const int* __restrict__ counts, int cap, int n_img, long t, int& img, int& k)
+{
+    long acc = 0;
+    for (int i = 0; i < n_img; ++i) {
+        int c = counts[i];
+        if (c > cap) c = cap;
+        if (t < acc + c) { img = i; k = (int)(t - acc); return true; }
+        acc += c;
+    }
+    return false;
+}
+
+__device__ __forceinline__ long flat_total(const int* __restrict__ counts, int cap, int n_img)
+{
+    long acc = 0;
+    for (int i = 0; i < n_img; ++i) { int c = counts[i]; acc += c > cap ? cap : c; }
+    return acc;
+}
+
+#define DAT(p, P, y, x) ((p)[(size_t)(y) * (P) + (x)])
+
+// 3x3 Cramer solve in double (same expression tree as oracle solve3)
+__device__ __forceinline__ void solve3_dev(const float H[9], const float b[3], float X[3])
+{
+    double a00 = H[0], a01 = H[1], a02 = H[2], a10 = H[3], a11 = H[4], a12 = H[5], a20 = H[6], a21 = H[7], a22 = H[8];
+    double c00 = a11 * a22 - a12 * a21, c01 = a10 * a22 - a12 * a20, c02 = a10 * a21 - a11 * a20;
+    double det = a00 * c00 - a01 * c01 + a02 * c02;
+    if (det == 0.0) { X[0] = X[1] = X[2] = 0.0f; return; }
+    double b0 = b[0], b1 = b[1], b2 = b[2];
+    double x0 = b0 * c00 - a01 * (b1 * a22 - a12 * b2) + a02 * (b1 * a21 - a11 * b2);
+    double x1 = a00 * (b1 * a22 - a12 * b2) - b0 * c01 + a02 * (a10 * b2 - b1 * a20);
+    double x2 = a00 * (a11 * b2 - b1 * a21) - a01 * (a10 * b2 - b1 * a20) + b0 * c02;
+    double inv = 1.0 / det;
+    X[0] = (float)(x0 * inv); X[1] = (float)(x1 * inv); X[2] = (float)(x2 * inv);
+}
+
+__global__ __launch_bounds__(64) void k_refine_orient(const Pyramid* __restrict__ py, const float* __restrict__ arena,
+                                                      const uint32_t* __restrict__ cand, const int* __restrict__ n_cand,
+                                                      CandOut* __restrict__ cout, int cand_cap, int n_img,
+                                                      float contrast_thr, float edge_thr, float sigma)
+{
+    __shared__ unsigned long long hfx[VO_SIFT_ORI_BINS];
+    __shared__ float tf[VO_SIFT_ORI_BINS];
+    __shared__ float hs[VO_SIFT_ORI_BINS];
+    const int lane = threadIdx.x;
+    const int L = py->L;
+    const long total = flat_total(n_cand, cand_cap, n_img);
+    for (long t = blockIdx.x; t < total; t += gridDim.x) {
+        int img, kidx;
+        flat_item(n_cand, cand_cap, n_img, t, img, kidx);
+        const uint32_t pc = cand[(size_t)img * cand_cap + kidx];
+        const int c0 = pc & 4095, r0 = (pc >> 12) & 4095, layer0 = (pc >> 24) & 7, o = pc >> 27;
+        const OctGeom& g = py->oct[o];
+        const int rows = g.rows, cols = g.cols, P = g.pitch;
+        CandOut* out = cout + (size_t)img * cand_cap + kidx;
+        // ---- adjustLocalExtrema (wave-uniform) ----
+        const float img_scale = 1.0f / 255.0f;
+        const float ds = img_scale * 0.5f, ss = img_scale, cs = img_scale * 0.25f;
+        int r = r0, c = c0, layer = layer0;
+        float xi = 0, xr = 0, xc = 0;
+        int it = 0;
+        bool ok = true;
+        for (; it < VO_SIFT_MAX_INTERP; ++it) {
+            const float* im = arena + g.d_off[layer] + img * g.plane;
+            const float* pv = arena + g.d_off[layer - 1] + img * g.plane;
+            const float* nx = arena + g.d_off[layer + 1] + img * g.plane;
+            float dD[3] = {(DAT(im, P, r, c + 1) - DAT(im, P, r, c - 1)) * ds,
+                           (DAT(im, P, r + 1, c) - DAT(im, P, r - 1, c)) * ds,
+                           (DAT(nx, P, r, c) - DAT(pv, P, r, c)) * ds};
+            float v2 = DAT(im, P, r, c) * 2.0f;
+            float dxx = (DAT(im, P, r, c + 1) + DAT(im, P, r, c - 1) - v2) * ss;
+            float dyy = (DAT(im, P, r + 1, c) + DAT(im, P, r - 1, c) - v2) * ss;
+            float dss = (DAT(nx, P, r, c) + DAT(pv, P, r, c) - v2) * ss;
+            float dxy = (DAT(im, P, r + 1, c + 1) - DAT(im, P, r + 1, c - 1) - DAT(im, P, r - 1, c + 1) + DAT(im, P, r - 1, c - 1)) * cs;
+            float dxs = (DAT(nx, P, r, c + 1) - DAT(nx, P, r, c - 1) - DAT(pv, P, r, c + 1) + DAT(pv, P, r, c - 1)) * cs;
+            float dys = (DAT(nx, P, r + 1, c) - DAT(nx, P, r - 1, c) - DAT(pv, P, r + 1, c) + DAT(pv, P, r - 1, c)) * cs;
+            float H[9] = {dxx, dxy, dxs, dxy, dyy, dys, dxs, dys, dss};
+            float X[3];
+            solve3_dev(H, dD, X);
+            xi = -X[2]; xr = -X[1]; xc = -X[0];
+            if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
+            const float big = (float)(0x7fffffff / 3);
+            if (fabsf(xi) > big || fabsf(xr) > big || fabsf(xc) > big) { ok = false; break; }
+            c += vo_round(xc); r += vo_round(xr); layer += vo_round(xi);
+            if (layer < 1 || layer > L || c < VO_SIFT_BORDER || c >= cols - VO_SIFT_BORDER ||
+                r < VO_SIFT_BORDER || r >= rows - VO_SIFT_BORDER) { ok = false; break; }
+        }
+        if (it >= VO_SIFT_MAX_INTERP) ok = false;
+        float xo = 0, yo = 0, scl = 0, resp = 0;
+        if (ok) {
+            const float* im = arena + g.d_off[layer] + img * g.plane;
+            const float* pv = arena + g.d_off[layer - 1] + img * g.plane;
+            const float* nx = arena + g.d_off[layer + 1] + img * g.plane;
+            float dD[3] = {(DAT(im, P, r, c + 1) - DAT(im, P, r, c - 1)) * ds,
+                           (DAT(im, P, r + 1, c) - DAT(im, P, r - 1, c)) * ds,
+                           (DAT(nx, P, r, c) - DAT(pv, P, r, c)) * ds};
+            float tt = dD[0] * xc + dD[1] * xr + dD[2] * xi;
+            float contr = DAT(im, P, r, c) * img_scale + tt * 0.5f;
+            if (fabsf(contr) * (float)L < contrast_thr) ok = false;
+            float v2 = DAT(im, P, r, c) * 2.0f;
+            float dxx = (DAT(im, P, r, c + 1) + DAT(im, P, r, c - 1) - v2) * ss;
+            float dyy = (DAT(im, P, r + 1, c) + DAT(im, P, r - 1, c) - v2) * ss;
+            float dxy = (DAT(im, P, r + 1, c + 1) - DAT(im, P, r + 1, c - 1) - DAT(im, P, r - 1, c + 1) + DAT(im, P, r - 1, c - 1)) * cs;
+            float tr = dxx + dyy, det = dxx * dyy - dxy * dxy;
+            if (det <= 0 || tr * tr * edge_thr >= (edge_thr + 1) * (edge_thr + 1) * det) ok = false;
+            xo = (float)c + xc;
+            yo = (float)r + xr;
+            scl = sigma * vo_expf(((float)layer + xi) / (float)L * 0.693147181f);
+            resp = fabsf(contr);
+        }
+        if (!ok) {
+            if (lane == 0) out->npk = 0;
+            continue;
+        }
+        // ---- orientation histogram ----
+        const float* gim = arena + g.g_off[layer] + img * g.plane;
+        const int radius = vo_round(VO_SIFT_ORI_RADIUS * scl);
+        const float sigw = VO_SIFT_ORI_SIG * scl;
+        const float expf_scale = -1.0f / (2.0f * sigw * sigw);
+        if (lane < VO_SIFT_ORI_BINS) hfx[lane] = 0ull;
+        __syncthreads();
+        const int side = 2 * radius + 1, nsamp = side * side;
+        for (int s = lane; s < nsamp; s += 64) {
+            const int i = s / side - radius, j = s - (s / side) * side - radius;
+            const int y = r + i, x = c + j;
+            if (y <= 0 || y >= rows - 1 || x <= 0 || x >= cols - 1) continue;
+            float dx = DAT(gim, P, y, x + 1) - DAT(gim, P, y, x - 1);
+            float dy = DAT(gim, P, y - 1, x) - DAT(gim, P, y + 1, x);
+            float w = vo_expf((float)(i * i + j * j) * expf_scale);
+            float mag = sqrtf(dx * dx + dy * dy);
+            float ori = vo_atan2_deg(dy, dx);
+            int bin = vo_round((float)VO_SIFT_ORI_BINS / 360.0f * ori);
+            if (bin >= VO_SIFT_ORI_BINS) bin -= VO_SIFT_ORI_BINS;
+            if (bin < 0) bin += VO_SIFT_ORI_BINS;
+            atomicAdd(&hfx[bin], (unsigned long long)(long long)vo_fx_quant(w * mag));
+        }
+        __syncthreads();
+        if (lane < VO_SIFT_ORI_BINS) tf[lane] = vo_fx_to_float((int64_t)hfx[lane]);
+        __syncthreads();
+        const int n = VO_SIFT_ORI_BINS;
+        float hv = -INFINITY;
+        if (lane < n) {
+            float m2 = tf[(lane + n - 2) % n], m1 = tf[(lane + n - 1) % n], p1 = tf[(lane + 1) % n], p2 = tf[(lane + 2) % n];
+            hv = (m2 + p2) * (1.0f / 16.0f) + (m1 + p1) * (4.0f / 16.0f) + tf[lane] * (6.0f / 16.0f);
+            hs[lane] = hv;
+        }
+        float mx = hv;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+        __syncthreads();
+        const float mag_thr = mx * VO_SIFT_ORI_PEAK;
+        bool pk = false;
+        float ang = 0.0f;
+        if (lane < n) {
+            const int l = lane > 0 ? lane - 1 : n - 1, r2 = lane < n - 1 ? lane + 1 : 0;
+            const float hl = hs[l], hr = hs[r2];
+            if (hv > hl && hv > hr && hv >= mag_thr) {
+                pk = true;
+                float bin = (float)lane + 0.5f * (hl - hr) / (hl - 2.0f * hv + hr);
+                bin = bin < 0 ? (float)n + bin : bin >= (float)n ? bin - (float)n : bin;
+                ang = 360.0f - (360.0f / (float)n) * bin;
+                if (fabsf(ang - 360.0f) < VO_FLT_EPSILON) ang = 0.0f;
+            }
+        }
+        const unsigned long long bal = __ballot(pk);
+        if (pk) {
+            const int rank = __popcll(bal & ((1ull << lane) - 1ull));
+            out->ang[rank] = ang;
+        }
+        if (lane == 0) {
+            out->xo = xo; out->yo = yo; out->scl = scl; out->response = resp;
+            out->o = o; out->layer = layer; out->r = r; out->c = c;
+            out->npk = __popcll(bal);
+        }
+        __syncthreads();
+    }
+}
+
+// per image exclusive scan of npk -> koff, n_kp. grid n_img, block 1024
+__global__ __launch_bounds__(1024) void k_scan_cands(const CandOut* __restrict__ cout, const int* __restrict__ n_cand,
+                                                     uint32_t* __restrict__ koff, int* __restrict__ n_kp, int cand_cap)
+{
+    __shared__ uint32_t sh[32];
+    const int img = blockIdx.x, tid = threadIdx.x;
+    int n = n_cand[img];
+    if (n > cand_cap) n = cand_cap;
+    const CandOut* co = cout + (size_t)img * cand_cap;
+    uint32_t* ko = koff + (size_t)img * cand_cap;
+    const int chunk = (n + 1023) / 1024;
+    const int a = tid * chunk, e = min(a + chunk, n);
+    uint32_t s = 0;
+    for (int k = a; k < e; ++k) s += (uint32_t)co[k].npk;
+    uint32_t total;
+    uint32_t base = block_exscan_1024(s, sh, &total);
+    for (int k = a; k < e; ++k) { ko[k] = base; base += (uint32_t)co[k].npk; }
+    if (tid == 0) n_kp[img] = (int)total;
+}
+
+__global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict__ n_cand, const uint32_t* __restrict__ koff,
+                         vo_keypoint* __restrict__ kp, KpInt* __restrict__ kpi, int cand_cap, int kp_cap, int n_img,
+                         int upsample)
+{
+    const long total = flat_total(n_cand, cand_cap, n_img);
+    for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+        int img, k;
+        flat_item(n_cand, cand_cap, n_img, t, img, k);
+        const CandOut& co = cout[(size_t)img * cand_cap + k];
+        const int npk = co.npk;
+        if (!npk) continue;
+        const uint32_t base = koff[(size_t)img * cand_cap + k];
+        const float oscale = (float)(1 << co.o) * (upsample ? 0.5f : 1.0f);
+        for (int p = 0; p < npk; ++p) {
+            const uint32_t idx = base + p;
+            if (idx >= (uint32_t)kp_cap) break;
+            vo_keypoint q;
+            q.x = co.xo * oscale + 1.0f;
+            q.y = co.yo * oscale + 1.0f;
+            q.size = co.scl * 2.0f * oscale;
+            q.angle = co.ang[p];
+            q.response = co.response;
+            q.octave = co.o - (upsample ? 1 : 0);
+            q.layer = co.layer;
+            q.scale = co.scl * oscale;
+            kp[(size_t)img * kp_cap + idx] = q;
+            KpInt qi;
+            qi.xo = co.xo; qi.yo = co.yo; qi.scl = co.scl; qi.angle = co.ang[p];
+            qi.o = co.o; qi.layer = co.layer; qi.pad0 = 0; qi.pad1 = 0;
+            kpi[(size_t)img * kp_cap + idx] = qi;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// descriptor: one wave (block of 64) per keypoint
+// ---------------------------------------------------------------------------
+#define DW VO_SIFT_DESCR_W
+#define DN VO_SIFT_DESCR_BINS
+#define DHIST ((DW + 2) * (DW + 2) * (DN + 2))
+
+__global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
+                                             const KpInt* __restrict__ kpi, const int* __restrict__ n_kp,
+                                             uint8_t* __restrict__ desc, DescMeta* __restrict__ meta, int kp_cap, int n_img)
+{
+    __shared__ unsigned long long hfx[DHIST];
+    const int lane = threadIdx.x;
+    const long total = flat_total(n_kp, kp_cap, n_img);
+    for (long t = blockIdx.x; t < total; t += gridDim.x) {
+        int img, k;
+        flat_item(n_kp, kp_cap, n_img, t, img, k);
+        const KpInt q = kpi[(size_t)img * kp_cap + k];
+        const OctGeom& g = py->oct[q.o];
+        const int rows = g.rows, cols = g.cols, P = g.pitch;
+        const float* gim = arena + g.g_off[q.layer] + img * g.plane;
+        for (int b = lane; b < DHIST; b += 64) hfx[b] = 0ull;
+        float ori = 360.0f - q.angle;
+        if (fabsf(ori - 360.0f) < VO_FLT_EPSILON) ori = 0.0f;
+        const int px = vo_round(q.xo), pyy = vo_round(q.yo);
+        float sin_t, cos_t;
+        vo_sincos_deg(ori, &sin_t, &cos_t);
+        const float bins_per_deg = (float)DN / 360.0f;
+        const float exp_scale = -1.0f / ((float)(DW * DW) * 0.5f);
+        const float hist_width = VO_SIFT_DESCR_SCL * q.scl;
+        int radius = vo_round(hist_width * 1.4142135623730951f * (float)(DW + 1) * 0.5f);
+        const int rmax = (int)sqrt((double)cols * cols + (double)rows * rows);
+        if (radius > rmax) radius = rmax;
+        cos_t = cos_t / hist_width;
+        sin_t = sin_t / hist_width;
+        __syncthreads();
+        const int side = 2 * radius + 1, nsamp = side * side;
+        for (int s = lane; s < nsamp; s += 64) {
+            const int i = s / side - radius, j = s - (s / side) * side - radius;
+            float c_rot = (float)j * cos_t - (float)i * sin_t;
+            float r_rot = (float)j * sin_t + (float)i * cos_t;
+            float rbin = r_rot + (float)(DW / 2) - 0.5f;
+            float cbin = c_rot + (float)(DW / 2) - 0.5f;
+            const int r = pyy + i, c = px + j;
+            if (!(rbin > -1.0f && rbin < (float)DW && cbin > -1.0f && cbin < (float)DW &&
+                  r > 0 && r < rows - 1 && c > 0 && c < cols - 1)) continue;
+            float dx = DAT(gim, P, r, c + 1) - DAT(gim, P, r, c - 1);
+            float dy = DAT(gim, P, r - 1, c) - DAT(gim, P, r + 1, c);
+            float w = vo_expf((c_rot * c_rot + r_rot * r_rot) * exp_scale);
+            float ang = vo_atan2_deg(dy, dx);
+            float mag = sqrtf(dx * dx + dy * dy) * w;
+            float obin = (ang - ori) * bins_per_deg;
+            int r0 = vo_floor(rbin), c0 = vo_floor(cbin), o0 = vo_floor(obin);
+            rbin -= (float)r0; cbin -= (float)c0; obin -= (float)o0;
+            if (o0 < 0) o0 += DN;
+            if (o0 >= DN) o0 -= DN;
+            float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+            float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+            float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+            float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+            float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+            float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+            float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+            const int idx = ((r0 + 1) * (DW + 2) + c0 + 1) * (DN + 2) + o0;
+            atomicAdd(&hfx[idx], (unsigned long long)(long long)vo_fx_quant(v_rco000));
+            atomicAdd(&hfx[idx + 1], (unsigned long long)(long long)vo_fx_quant(v_rco001));
+            atomicAdd(&hfx[idx + (DN + 2)], (unsigned long long)(long long)vo_fx_quant(v_rco010));
+            atomicAdd(&hfx[idx + (DN + 3)], (unsigned long long)(long long)vo_fx_quant(v_rco011));
+            atomicAdd(&hfx[idx + (DW + 2) * (DN + 2)], (unsigned long long)(long long)vo_fx_quant(v_rco100));
+            atomicAdd(&hfx[idx + (DW + 2) * (DN + 2) + 1], (unsigned long long)(long long)vo_fx_quant(v_rco101));
+            atomicAdd(&hfx[idx + (DW + 3) * (DN + 2)], (unsigned long long)(long long)vo_fx_quant(v_rco110));
+            atomicAdd(&hfx[idx + (DW + 3) * (DN + 2) + 1], (unsigned long long)(long long)vo_fx_quant(v_rco111));
+        }
+        __syncthreads();
+        // fold the circular orientation bins and convert; lane holds dst[lane], dst[lane+64]
+        float dv[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int kk = lane + 64 * h;
+            const int cell = kk / DN, ob = kk - cell * DN;
+            const int ci = cell / DW, cj = cell - ci * DW;
+            const int base = ((ci + 1) * (DW + 2) + (cj + 1)) * (DN + 2);
+            long long v = (long long)hfx[base + ob];
+            if (ob < 2) v += (long long)hfx[base + DN + ob];
+            dv[h] = vo_fx_to_float((int64_t)v);
+        }
+        float s = dv[0] * dv[0] + dv[1] * dv[1];
+#pragma unroll
+        for (int st = 32; st >= 1; st >>= 1) s = s + __shfl_down(s, st);
+        const float nrm0 = __shfl(s, 0);
+        const float thr = sqrtf(nrm0) * VO_SIFT_DESCR_MAG_THR;
+        dv[0] = dv[0] < thr ? dv[0] : thr;
+        dv[1] = dv[1] < thr ? dv[1] : thr;
+        s = dv[0] * dv[0] + dv[1] * dv[1];
+#pragma unroll
+        for (int st = 32; st >= 1; st >>= 1) s = s + __shfl_down(s, st);
+        const float nrm = sqrtf(__shfl(s, 0));
+        const float scale = VO_SIFT_DESCR_INT_FCTR / (nrm > VO_FLT_EPSILON ? nrm : VO_FLT_EPSILON);
+        int qv[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            float v = rintf(dv[h] * scale);
+            qv[h] = v < 0.0f ? 0 : v > 255.0f ? 255 : (int)v;
+        }
+        uint8_t* dst = desc + ((size_t)img * kp_cap + k) * VO_DESC_LEN;
+        dst[lane] = (uint8_t)qv[0];
+        dst[lane + 64] = (uint8_t)qv[1];
+        int sum = qv[0] + qv[1], sq = qv[0] * qv[0] + qv[1] * qv[1];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) { sum += __shfl_xor(sum, off); sq += __shfl_xor(sq, off); }
+        if (lane == 0) {
+            DescMeta m;
+            m.sum = sum;
+            m.inv_norm = sq > 0 ? 1.0f / sqrtf((float)sq) : 0.0f;
+            meta[(size_t)img * kp_cap + k] = m;
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host enqueue
+// ---------------------------------------------------------------------------
+static Kern make_kern(const Pyramid& py, int level)
+{
+    Kern k;
+    memset(&k, 0, sizeof(k));
+    k.r = py.krad[level];
+    for (int j = 0; j <= k.r; ++j) k.k[j] = py.kern[level][j];
+    return k;
+}
+
+void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img, const vo_sift_params& p,
+                  hipStream_t s, const Pyramid* d_py)
+{
+    const int L = py.L;
+    float* A = b.arena;
+    for (int o = 0; o < py.n_oct; ++o) {
+        const OctGeom& g = py.oct[o];
+        const int R = g.rows, C = g.cols;
+        dim3 gh((C + HB - 1) / HB, R, n_img), bh(HB);
+        dim3 gv((C + VT_W - 1) / VT_W, (R + VT_H - 1) / VT_H, n_img), bv(64, 4);
+        if (o == 0) {
+            Kern K0 = make_kern(py, 0);
+            const int rows = p.upsample ? R / 2 : R, cols = p.upsample ? C / 2 : C;
+            if (p.upsample) VO_LAUNCH(k_base_h<true>, gh, bh, 0, s, src, rows, cols, R, C, b.tmp, py.tmp_plane, g.pitch, K0);
+            else VO_LAUNCH(k_base_h<false>, gh, bh, 0, s, src, rows, cols, R, C, b.tmp, py.tmp_plane, g.pitch, K0);
+            VO_LAUNCH(k_blur_v<false>, gv, bv, 0, s, b.tmp, py.tmp_plane, g.pitch, R, C, A + g.g_off[0],
+                               (const float*)nullptr, (float*)nullptr, g.plane, K0);
+        } else {
+            const OctGeom& pg = py.oct[o - 1];
+            size_t n = (size_t)n_img * R * C;
+            int blocks = (int)((n + 255) / 256);
+            if (blocks > 4096) blocks = 4096;
+            if (blocks < 1) blocks = 1;
+            VO_LAUNCH(k_down, dim3(blocks), dim3(256), 0, s, A + pg.g_off[L], pg.plane, pg.pitch, A + g.g_off[0],
+                               g.plane, g.pitch, R, C, n_img);
+        }
+        for (int i = 1; i < L + 3; ++i) {
+            Kern K = make_kern(py, i);
+            VO_LAUNCH(k_blur_h, gh, bh, 0, s, A + g.g_off[i - 1], g.plane, g.pitch, R, C, b.tmp, py.tmp_plane, K);
+            VO_LAUNCH(k_blur_v<true>, gv, bv, 0, s, b.tmp, py.tmp_plane, g.pitch, R, C, A + g.g_off[i],
+                               A + g.g_off[i - 1], A + g.d_off[i - 1], g.plane, K);
+        }
+    }
+    const float thr = (float)floor(0.5 * p.contrast_threshold / L * 255.0);
+    long words = (long)py.n_words * n_img;
+    int eb = (int)((words + 3) / 4);
+    if (eb > 8192) eb = 8192;
+    if (eb < 1) eb = 1;
+    VO_LAUNCH(k_ext_mask, dim3(eb), dim3(256), 0, s, d_py, A, b.mask, n_img, thr);
+    VO_LAUNCH(k_scan_words, dim3(n_img), dim3(1024), 0, s, b.mask, b.woff, b.n_cand, py.n_words);
+    int mb = (int)((words + 255) / 256);
+    if (mb > 4096) mb = 4096;
+    if (mb < 1) mb = 1;
+    VO_LAUNCH(k_emit, dim3(mb), dim3(256), 0, s, d_py, b.mask, b.woff, b.cand, b.cand_cap, n_img);
+    VO_LAUNCH(k_refine_orient, dim3(8192), dim3(64), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.cand_cap, n_img,
+                       p.contrast_threshold, p.edge_threshold, p.sigma);
+    VO_LAUNCH(k_scan_cands, dim3(n_img), dim3(1024), 0, s, b.cout, b.n_cand, b.koff, b.n_kp, b.cand_cap);
+    VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, b.n_cand, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
+                       n_img, p.upsample);
+    VO_LAUNCH(k_desc, dim3(8192), dim3(64), 0, s, d_py, A, b.kpi, b.n_kp, b.desc, b.meta, b.kp_cap, n_img);
+}
+
+}  // namespace vo

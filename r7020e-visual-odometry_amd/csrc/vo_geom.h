@@ -1,0 +1,84 @@
+// vo_geom.h — device buffers and launchers for the tracking + geometry part of
+// the per-frame path: find_remaining_points (VO.m:280-334) as index
+// composition over match jobs, DLT triangulation (VO.m:113-116), P3P + MSAC
+// (VO.m:123-127), and the landmark filter / CreateLandmarksFromFeatures
+// (VO.m:145-160).  All batched over the frames of a call.
+#pragma once
+#include "vo_internal.h"
+
+namespace vo {
+
+// index lists per frame (each [kp_cap] ints), see geom.hip for the sequence
+enum TrackList {
+    TL_OL1, TL_OR1, TL_CL, TL_OL2, TL_OR2, TL_CR, TL_CL2, TL_CR2, TL_OLF, TL_ORF, TL_CLF, TL_CRF, TL_COUNT
+};
+
+struct MsacHyp {
+    double R[9];
+    double t[3];
+    double score;
+    int valid;
+    int n_in;
+};
+
+struct FrameGeom {
+    int status;
+    int n_inliers;
+    int best;
+    int n_tracked;
+    double T[16];          // rel_pose (camera pose of cur in prev frame)
+};
+
+struct GeomBuffers {
+    int max_frames = 0, kp_cap = 0, n_hyp = 0;
+    int* lists = nullptr;        // [max_frames][TL_COUNT][kp_cap]
+    int* list_n = nullptr;       // [max_frames][4]  n after lm, rm, cm, last
+    int* step_i = nullptr;       // [4][max_frames][kp_cap] match outputs
+    int* step_j = nullptr;
+    int* step_n = nullptr;       // [4][max_frames]
+    double* world = nullptr;     // [max_frames][kp_cap][3]
+    double* imgpt = nullptr;     // [max_frames][kp_cap][2]
+    float* oldpos = nullptr;     // [max_frames][kp_cap][4]  old left xy, old right xy
+    uint8_t* inliers = nullptr;  // [max_frames][kp_cap]
+    MsacHyp* hyp = nullptr;      // [max_frames][n_hyp]
+    FrameGeom* fg = nullptr;     // [max_frames]
+    // landmarks
+    int* lm_new = nullptr;       // [max_frames][kp_cap]  compacted indices of new stereo matches
+    int* lm_M = nullptr;         // [max_frames]
+    float* lm_X = nullptr;       // [max_frames][kp_cap][3] camera-frame points of odd rows
+    uint8_t* lm_keep = nullptr;  // [max_frames][kp_cap]
+    int* lm_rows = nullptr;      // [max_frames]
+};
+
+hipError_t geom_alloc(GeomBuffers& g, int max_frames, int kp_cap, int n_hyp);
+void geom_free(GeomBuffers& g);
+
+// Fill the 4 x max_frames tracking match jobs starting at jobs[first].
+// Frame f: cur images 2f (left) / 2f+1 (right); prev frame = f-1, frame 0's
+// prev is the carried frame (image slots 2*max_frames, 2*max_frames+1; pair
+// slot max_frames).
+void geom_fill_track_jobs(const GeomBuffers& g, MatchJob* jobs, int max_frames, int first, const SiftBuffers& sb,
+                          int* pair_i, int* pair_j, int* pair_n, int kp_cap);
+
+struct StepArgs {
+    const SiftBuffers* sb;
+    const int* pair_i; const int* pair_j; const int* pair_n;   // stereo pairs per pair slot
+    int max_frames, B, kp_cap;
+    int first_has_prev;            // frame 0 of this call has a previous frame (carry)
+    long frame_index0;             // global index of frame 0 (Philox key)
+    vo_calib calib;
+    vo_ransac_params rp;
+};
+
+// Enqueue tracking (4 matches + compositions), triangulation, MSAC and the
+// landmark kernels for frames [0, B).  match jobs at d_jobs + first.
+void geom_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_track_jobs, const StepArgs& a,
+                  const vo_match_params& mp, hipStream_t s);
+
+// Standalone launchers used by the single-call ABI functions.
+void triangulate_launch(const float* x1, const float* x2, int n, const double* P1, const double* P2, double* X,
+                        hipStream_t s);
+void estworldpose_launch(GeomBuffers& g, const double* img, const double* world, const int* n, const double K[9],
+                         const vo_ransac_params& rp, uint32_t frame_key, hipStream_t s);
+
+}  // namespace vo

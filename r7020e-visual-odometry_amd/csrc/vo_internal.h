@@ -1,0 +1,166 @@
+// vo_internal.h — device data layout and kernel launch interfaces of libvo.
+// Layout rationale: DESIGN.md §4.  All kernels are hand-written HIP for gfx950
+// (wave64), compiled with -ffp-contract=off so every float operation is the
+// IEEE basic op the spec (include/vo_spec.h) names.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <vector>
+#include <string>
+#include "vo.h"
+#include "vo_spec.h"
+
+#define VO_WAVE 64
+
+namespace vo {
+
+// ---------------------------------------------------------------------------
+// Per-kernel HIP-event timing (vo_set_profiling).  When enabled every launch
+// made through VO_LAUNCH is bracketed by two events on its stream; the
+// durations are summed per kernel name after the call synchronises.
+// ---------------------------------------------------------------------------
+struct Profiler {
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    int used = 0;
+    std::vector<std::pair<const char*, int>> marks;   // (kernel name, start event index)
+    std::vector<std::string> names;
+    std::vector<double> ms;
+    std::vector<int> calls;
+    void begin(const char* name, hipStream_t s);
+    void end(hipStream_t s);
+    void collect();      // after the stream has synchronised
+    void reset_totals();
+    ~Profiler();
+};
+extern Profiler* g_prof;
+
+#define VO_LAUNCH(kernel, grid, block, shmem, stream, ...)                                  \
+    do {                                                                                   \
+        if (::vo::g_prof && ::vo::g_prof->on) ::vo::g_prof->begin(#kernel, stream);        \
+        hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);               \
+        if (::vo::g_prof && ::vo::g_prof->on) ::vo::g_prof->end(stream);                   \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// Scale-space arena.  For each octave o and level i, the planes of all images
+// of a batch are contiguous: G(o,i,img) = arena + g_off[o][i] + img*plane[o].
+// Rows are padded to a multiple of 64 floats (256 B) so every row starts on a
+// cache-line boundary and a wave's 64 consecutive columns are one coalesced
+// 256-B access.
+// ---------------------------------------------------------------------------
+struct OctGeom {
+    int rows, cols, pitch;
+    int pad;
+    size_t plane;                       // rows * pitch (floats)
+    size_t g_off[VO_SIFT_MAX_LAYERS];   // L+3 Gaussian levels
+    size_t d_off[VO_SIFT_MAX_LAYERS];   // L+2 DoG levels
+};
+
+struct Pyramid {
+    int n_oct, L, n_img;
+    OctGeom oct[VO_SIFT_MAX_OCTAVES];
+    float kern[VO_SIFT_MAX_LAYERS][VO_SIFT_MAX_RADIUS + 1];  // level blur kernels (level 0 = base)
+    int krad[VO_SIFT_MAX_LAYERS];
+    size_t total;                        // floats in the arena
+    size_t tmp_plane;                    // floats per image of the horizontal-pass scratch
+    // extrema word layout: words of 64 interior columns per (octave, layer, row)
+    int wbase[VO_SIFT_MAX_OCTAVES * 4 + 1];   // prefix over (o, layer-1) blocks; size n_oct*L+1
+    int wrow[VO_SIFT_MAX_OCTAVES];            // words per row in octave o
+    int n_words;                              // words per image
+};
+
+// Packed candidate: c | r << 12 | layer << 24 | o << 27  (c, r < 4096)
+__host__ __device__ inline uint32_t pack_cand(int o, int layer, int r, int c) {
+    return (uint32_t)c | ((uint32_t)r << 12) | ((uint32_t)layer << 24) | ((uint32_t)o << 27);
+}
+
+// Refined candidate with its orientation peaks (output of refine_orient).
+struct CandOut {
+    float xo, yo, scl, response;
+    int o, layer, r, c;
+    int npk, pad0, pad1, pad2;
+    float ang[VO_SIFT_MAX_PEAKS + 2];
+};
+
+// Internal keypoint record used by the descriptor kernel.
+struct KpInt {
+    float xo, yo, scl, angle;
+    int o, layer, pad0, pad1;
+};
+
+// Per-descriptor metadata for matching: exact integer sums.
+struct DescMeta {
+    int32_t sum;      // sum of the 128 u8 values
+    float inv_norm;   // 1/sqrtf((float)sum of squares), 0 if zero
+};
+
+// Buffers of the SIFT stage for a batch of n_img images.
+struct SiftBuffers {
+    float* arena = nullptr;
+    float* tmp = nullptr;              // horizontal-pass scratch [n_img][tmp_plane]
+    unsigned long long* mask = nullptr;  // [n_img][n_words]
+    uint32_t* woff = nullptr;          // [n_img][n_words]
+    uint32_t* cand = nullptr;          // [n_img][cand_cap]
+    int* n_cand = nullptr;             // [n_img]  (uncapped count)
+    CandOut* cout = nullptr;           // [n_img][cand_cap]
+    uint32_t* koff = nullptr;          // [n_img][cand_cap]
+    int* n_kp = nullptr;               // [n_img]  (uncapped count)
+    vo_keypoint* kp = nullptr;         // [n_img][kp_cap]
+    KpInt* kpi = nullptr;              // [n_img][kp_cap]
+    uint8_t* desc = nullptr;           // [n_img][kp_cap][128]
+    DescMeta* meta = nullptr;          // [n_img][kp_cap]
+    int cand_cap = 0, kp_cap = 0, n_img = 0;
+};
+
+// Image source for the first octave: image i of the batch is
+// (i & 1 ? right : left) + (i >> 1) * frame_stride, row-major with ld.
+struct ImageSrc {
+    const uint8_t* left;
+    const uint8_t* right;
+    size_t frame_stride;
+    int ld;
+    int pad;
+};
+
+void build_pyramid_geometry(Pyramid& py, int rows, int cols, int n_img, const vo_sift_params& p);
+hipError_t sift_alloc(SiftBuffers& b, const Pyramid& py, int kp_cap, int cand_cap);
+void sift_free(SiftBuffers& b);
+// Enqueue the whole detect+describe pipeline for n_img images (<= allocated).
+// d_py is a device copy of py.
+void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img,
+                  const vo_sift_params& p, hipStream_t s, const Pyramid* d_py);
+
+// ---------------------------------------------------------------------------
+// Matching.  A match job compares F1 rows (desc[idx1[i]] for i < *n1) against
+// F2 rows.  idx == nullptr means identity.  Counts are read on device.
+// ---------------------------------------------------------------------------
+struct MatchJob {
+    const uint8_t* d1; const DescMeta* m1; const int* idx1; const int* n1;
+    const uint8_t* d2; const DescMeta* m2; const int* idx2; const int* n2;
+    int* out_i;      // [cap] F1 positions (0-based, position in the F1 list)
+    int* out_j;      // [cap] F2 positions
+    int* out_n;      // matches found
+    int cap;
+    int pad;
+};
+
+struct MatchTop2 { float best; int idx; float second; int pad; };
+
+struct MatchBuffers {
+    MatchJob* jobs = nullptr;        // device copy of the jobs [max_jobs]
+    MatchTop2* partial = nullptr;    // [max_jobs][n_chunks][row_cap]
+    int max_jobs = 0, row_cap = 0, n_chunks = 0;
+};
+
+#define VO_MATCH_CHUNK 512           // F2 columns per wave task
+
+hipError_t match_alloc(MatchBuffers& b, int max_jobs, int row_cap);
+void match_free(MatchBuffers& b);
+// d_jobs: device array of n_jobs jobs (prepared once per context); job k uses
+// partial-result slot k.
+void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, const vo_match_params& p,
+                  hipStream_t s);
+void desc_meta_launch(const uint8_t* desc, DescMeta* meta, int n, hipStream_t s);
+
+}  // namespace vo

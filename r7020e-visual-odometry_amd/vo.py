@@ -1,0 +1,313 @@
+"""Python host mirror of the reference's per-frame call surface, over the
+libvo C-ABI (include/vo.h).
+
+The reference (VO.m) calls MathWorks toolbox functions; this module exposes
+the same names with the same argument meaning and error behaviour, each
+running on the MI355X through libvo.so:
+
+    detectSIFTFeatures / extractFeatures   VO.m:79-84
+    matchFeatures                          VO.m:87,283,293,311,323
+    find_remaining_points                  VO.m:280-334
+    triangulate                            VO.m:113-116
+    estworldpose                           VO.m:123-127
+    CreateLandmarksFromFeatures            CreateLandmarksFromFeatures.m:1-21
+    VisualOdometry.step                    the VO.m loop body (VO.m:70-161)
+
+Coordinates are MATLAB 1-based.  Index pairs are 1-based uint32 (P x 2).
+There is no CPU fallback: if libvo.so cannot be loaded or no GPU is present,
+every call raises VOError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG = Path(__file__).resolve().parent
+LIBPATH = PKG / "lib" / "libvo.so"
+
+VO_OK = 0
+VO_ERR_ARG = -1
+VO_ERR_HIP = -2
+VO_ERR_TOO_FEW_POINTS = -3
+VO_ERR_NO_CONSENSUS = -4
+VO_ERR_CAPACITY = -5
+VO_ERR_STATE = -6
+
+
+class VOError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libvo error {code}: {msg}")
+        self.code = code
+
+
+class SiftParams(C.Structure):
+    _fields_ = [("n_octave_layers", C.c_int32), ("sigma", C.c_float), ("contrast_threshold", C.c_float),
+                ("edge_threshold", C.c_float), ("upsample", C.c_int32), ("max_keypoints", C.c_int32)]
+
+
+class MatchParams(C.Structure):
+    _fields_ = [("match_threshold", C.c_float), ("max_ratio", C.c_float)]
+
+
+class RansacParams(C.Structure):
+    _fields_ = [("max_num_trials", C.c_int32), ("confidence", C.c_double),
+                ("max_reprojection_error", C.c_double), ("seed", C.c_uint32)]
+
+
+class Calib(C.Structure):
+    _fields_ = [("P1", C.c_double * 12), ("P2", C.c_double * 12), ("K", C.c_double * 9)]
+
+
+class Keypoint(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("size", C.c_float), ("angle", C.c_float),
+                ("response", C.c_float), ("octave", C.c_int32), ("layer", C.c_int32), ("scale", C.c_float)]
+
+
+class StepOut(C.Structure):
+    _fields_ = [("status", C.c_int32), ("n_left", C.c_int32), ("n_right", C.c_int32),
+                ("n_stereo", C.c_int32), ("n_tracked", C.c_int32), ("n_inliers", C.c_int32),
+                ("n_landmarks", C.c_int32), ("pad", C.c_int32),
+                ("rel_pose", C.c_double * 16), ("pose", C.c_double * 16)]
+
+
+class PairStats(C.Structure):
+    _fields_ = [("n_left", C.c_int32), ("n_right", C.c_int32), ("n_stereo", C.c_int32), ("flags", C.c_int32)]
+
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+                     ("octave", "<i4"), ("layer", "<i4"), ("scale", "<f4")])
+STEP_DTYPE = np.dtype([("status", "<i4"), ("n_left", "<i4"), ("n_right", "<i4"), ("n_stereo", "<i4"),
+                       ("n_tracked", "<i4"), ("n_inliers", "<i4"), ("n_landmarks", "<i4"), ("pad", "<i4"),
+                       ("rel_pose", "<f8", (4, 4)), ("pose", "<f8", (4, 4))])
+
+# exported symbols (tests check the library exports every one)
+EXPORTS = [
+    "vo_default_sift_params", "vo_default_match_params", "vo_default_ransac_params", "vo_create", "vo_destroy",
+    "vo_set_calib", "vo_last_error", "vo_sift", "vo_match", "vo_track", "vo_triangulate", "vo_estworldpose",
+    "vo_landmarks", "vo_step", "vo_step_batch", "vo_step_batch_dev", "vo_get_landmarks", "vo_reset",
+    "vo_sift_match_batch_dev", "vo_fetch_keypoints", "vo_fetch_stereo_pairs", "vo_stream", "vo_set_profiling",
+    "vo_kernel_times",
+]
+
+_lib = None
+
+
+def load_library(path: str | os.PathLike | None = None):
+    """Load libvo.so (built in-tree by __graft_entry__.build()).  Raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = Path(path) if path else LIBPATH
+    if not p.exists():
+        raise VOError(VO_ERR_STATE, f"{p} not built; run __graft_entry__.build() (make -C csrc)")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same
+    # soname as /opt/rocm's).  Loading torch first makes libvo bind to that
+    # runtime, so device pointers from torch tensors and torch.distributed
+    # (RCCL) share one runtime with libvo.  Without torch, libvo uses /opt/rocm.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = C.CDLL(str(p))
+    P = C.POINTER
+    vp = C.c_void_p
+    L.vo_default_sift_params.argtypes = [P(SiftParams)]
+    L.vo_default_match_params.argtypes = [P(MatchParams)]
+    L.vo_default_ransac_params.argtypes = [P(RansacParams)]
+    L.vo_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, P(Calib), P(SiftParams), P(MatchParams), P(RansacParams)]
+    L.vo_create.restype = vp
+    L.vo_destroy.argtypes = [vp]
+    L.vo_destroy.restype = None
+    L.vo_set_calib.argtypes = [vp, P(Calib)]
+    L.vo_last_error.argtypes = [vp]
+    L.vo_last_error.restype = C.c_char_p
+    L.vo_sift.argtypes = [vp, P(C.c_uint8), C.c_int, C.c_int, C.c_int, P(Keypoint), P(C.c_uint8), C.c_int, P(C.c_int)]
+    L.vo_match.argtypes = [vp, P(C.c_uint8), C.c_int, P(C.c_uint8), C.c_int, P(C.c_uint32), C.c_int, P(C.c_int)]
+    L.vo_track.argtypes = [vp, P(C.c_uint8), P(C.c_uint8), C.c_int, P(C.c_uint8), C.c_int, P(C.c_uint8), C.c_int,
+                           P(C.c_uint32), C.c_int, P(C.c_int)]
+    L.vo_triangulate.argtypes = [vp, P(C.c_float), P(C.c_float), C.c_int, P(C.c_double), P(C.c_double), P(C.c_double)]
+    L.vo_estworldpose.argtypes = [vp, P(C.c_double), P(C.c_double), C.c_int, P(C.c_double), P(RansacParams),
+                                  C.c_uint32, P(C.c_double), P(C.c_uint8), P(C.c_int)]
+    L.vo_landmarks.argtypes = [vp, P(C.c_float), P(C.c_float), C.c_int, P(C.c_float), P(C.c_float), C.c_int,
+                               P(C.c_double), P(C.c_double), C.c_int, P(C.c_int)]
+    L.vo_step.argtypes = [vp, P(C.c_uint8), P(C.c_uint8), C.c_int, P(StepOut)]
+    L.vo_step_batch.argtypes = [vp, P(C.c_uint8), P(C.c_uint8), C.c_int, C.c_int, P(StepOut)]
+    L.vo_step_batch_dev.argtypes = [vp, vp, vp, C.c_int, P(StepOut)]
+    L.vo_get_landmarks.argtypes = [vp, P(C.c_double), C.c_int, P(C.c_int)]
+    L.vo_reset.argtypes = [vp]
+    L.vo_sift_match_batch_dev.argtypes = [vp, vp, vp, C.c_int, P(PairStats)]
+    L.vo_fetch_keypoints.argtypes = [vp, C.c_int, P(Keypoint), P(C.c_uint8), C.c_int, P(C.c_int)]
+    L.vo_fetch_stereo_pairs.argtypes = [vp, C.c_int, P(C.c_uint32), C.c_int, P(C.c_int)]
+    L.vo_stream.argtypes = [vp]
+    L.vo_stream.restype = vp
+    L.vo_set_profiling.argtypes = [vp, C.c_int]
+    L.vo_kernel_times.argtypes = [vp, P(C.c_char_p), P(C.c_double), P(C.c_int), C.c_int, P(C.c_int)]
+    _lib = L
+    return L
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def default_sift_params(max_keypoints: int = 16384) -> SiftParams:
+    p = SiftParams()
+    load_library().vo_default_sift_params(C.byref(p))
+    p.max_keypoints = max_keypoints
+    return p
+
+
+def default_match_params() -> MatchParams:
+    p = MatchParams()
+    load_library().vo_default_match_params(C.byref(p))
+    return p
+
+
+def default_ransac_params() -> RansacParams:
+    p = RansacParams()
+    load_library().vo_default_ransac_params(C.byref(p))
+    return p
+
+
+def calib_from(P1, P2, K=None) -> Calib:
+    c = Calib()
+    c.P1[:] = [float(v) for v in np.asarray(P1, np.float64).reshape(-1)]
+    c.P2[:] = [float(v) for v in np.asarray(P2, np.float64).reshape(-1)]
+    K = np.asarray(P1, np.float64)[:, :3] if K is None else np.asarray(K, np.float64)
+    c.K[:] = [float(v) for v in K.reshape(-1)]
+    return c
+
+
+class Context:
+    """One libvo context (one HIP device, fixed image size, up to max_batch frames per call)."""
+
+    def __init__(self, rows: int = 375, cols: int = 1242, max_batch: int = 1, device: int = 0, calib: Calib | None = None,
+                 sift: SiftParams | None = None, match: MatchParams | None = None, ransac: RansacParams | None = None):
+        self.lib = load_library()
+        self.rows, self.cols, self.max_batch = rows, cols, max_batch
+        self.sift_params = sift or default_sift_params()
+        self.match_params = match or default_match_params()
+        self.ransac_params = ransac or default_ransac_params()
+        h = self.lib.vo_create(device, rows, cols, max_batch, C.byref(calib) if calib else None,
+                               C.byref(self.sift_params), C.byref(self.match_params), C.byref(self.ransac_params))
+        if not h:
+            raise VOError(VO_ERR_HIP, self.lib.vo_last_error(None).decode())
+        self.h = C.c_void_p(h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.vo_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, allow=()):
+        if rc != VO_OK and rc not in allow:
+            raise VOError(rc, self.lib.vo_last_error(self.h).decode())
+        return rc
+
+    # ---- detectSIFTFeatures + extractFeatures ----
+    def sift(self, img: np.ndarray):
+        img = np.ascontiguousarray(img, np.uint8)
+        cap = self.sift_params.max_keypoints
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 128), np.uint8)
+        n = C.c_int(0)
+        self._check(self.lib.vo_sift(self.h, _p(img, C.c_uint8), img.shape[0], img.shape[1], img.strides[0],
+                                     kps.ctypes.data_as(C.POINTER(Keypoint)), _p(desc, C.c_uint8), cap, C.byref(n)))
+        return kps[: n.value].copy(), desc[: n.value].copy()
+
+    # ---- matchFeatures ----
+    def match(self, F1: np.ndarray, F2: np.ndarray) -> np.ndarray:
+        F1 = np.ascontiguousarray(F1, np.uint8)
+        F2 = np.ascontiguousarray(F2, np.uint8)
+        cap = max(F1.shape[0], 1)
+        pairs = np.zeros((cap, 2), np.uint32)
+        n = C.c_int(0)
+        self._check(self.lib.vo_match(self.h, _p(F1, C.c_uint8), F1.shape[0], _p(F2, C.c_uint8), F2.shape[0],
+                                      _p(pairs, C.c_uint32), cap, C.byref(n)))
+        return pairs[: n.value].copy()
+
+    # ---- benchmark workload: SIFT + stereo match of B pairs resident on device ----
+    def sift_match_batch_dev(self, d_lefts: int, d_rights: int, B: int, stats: bool = True):
+        st = (PairStats * B)() if stats else None
+        self._check(self.lib.vo_sift_match_batch_dev(self.h, C.c_void_p(d_lefts), C.c_void_p(d_rights), B, st))
+        if stats:
+            return [(s.n_left, s.n_right, s.n_stereo, s.flags) for s in st]
+        return None
+
+    def fetch_keypoints(self, image: int):
+        cap = self.sift_params.max_keypoints
+        kps = np.zeros(cap, KP_DTYPE)
+        desc = np.zeros((cap, 128), np.uint8)
+        n = C.c_int(0)
+        self._check(self.lib.vo_fetch_keypoints(self.h, image, kps.ctypes.data_as(C.POINTER(Keypoint)),
+                                                _p(desc, C.c_uint8), cap, C.byref(n)))
+        m = min(n.value, cap)
+        return kps[:m].copy(), desc[:m].copy()
+
+    def fetch_stereo_pairs(self, frame: int) -> np.ndarray:
+        cap = self.sift_params.max_keypoints
+        pairs = np.zeros((cap, 2), np.uint32)
+        n = C.c_int(0)
+        self._check(self.lib.vo_fetch_stereo_pairs(self.h, frame, _p(pairs, C.c_uint32), cap, C.byref(n)))
+        return pairs[: min(n.value, cap)].copy()
+
+    # ---- profiling ----
+    def set_profiling(self, on: bool):
+        self._check(self.lib.vo_set_profiling(self.h, 1 if on else 0))
+
+    def kernel_times(self) -> dict:
+        n = C.c_int(0)
+        self._check(self.lib.vo_kernel_times(self.h, None, None, None, 0, C.byref(n)))
+        m = n.value
+        names = (C.c_char_p * m)()
+        ms = (C.c_double * m)()
+        calls = (C.c_int * m)()
+        self._check(self.lib.vo_kernel_times(self.h, names, ms, calls, m, C.byref(n)))
+        return {names[i].decode(): (ms[i], calls[i]) for i in range(m)}
+
+    def stream(self) -> int:
+        return self.lib.vo_stream(self.h) or 0
+
+
+# ---------------------------------------------------------------------------
+# MATLAB-named functional API (one shared default context per image size)
+# ---------------------------------------------------------------------------
+_ctx_cache: dict = {}
+
+
+def _default_ctx(rows: int, cols: int) -> Context:
+    key = (rows, cols)
+    if key not in _ctx_cache:
+        _ctx_cache[key] = Context(rows, cols, 1)
+    return _ctx_cache[key]
+
+
+def detectSIFTFeatures(I: np.ndarray):
+    """detectSIFTFeatures(I) (VO.m:79-80) fused with its descriptor pass: returns
+    (points, descriptors) where points is a structured array with MATLAB
+    1-based Location (x, y), Scale, Orientation (angle), Metric (response)."""
+    return _default_ctx(*I.shape).sift(I)
+
+
+def extractFeatures(I: np.ndarray, points=None, Method: str = "SIFT"):
+    """extractFeatures(I, points, "Method", "SIFT") (VO.m:83-84) -> (features, validPoints).
+    SIFT descriptors are computed in the same device pass as detection; all
+    points are valid."""
+    if Method != "SIFT":
+        raise VOError(VO_ERR_ARG, "only Method 'SIFT' is on the hot path")
+    kps, desc = _default_ctx(*I.shape).sift(I)
+    return desc, kps
+
+
+def matchFeatures(features1: np.ndarray, features2: np.ndarray) -> np.ndarray:
+    """matchFeatures defaults (Exhaustive, SSD, MatchThreshold 1, MaxRatio 0.6)."""
+    return _default_ctx(375, 1242).match(features1, features2)

@@ -1,0 +1,58 @@
+"""GPU parity: SIFT detect+describe and stereo matchFeatures through libvo.so
+vs the CPU oracle, bit for bit (keypoint records, descriptors, index pairs)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _same_kps(a, b):
+    assert len(a) == len(b), (len(a), len(b))
+    for f in ("x", "y", "size", "angle", "response", "octave", "layer", "scale"):
+        assert np.array_equal(a[f], b[f]), f
+
+
+def test_sift_single_image_bit_exact(vo, oracle, syn):
+    L, R = syn.stereo_pair(syn.SEED_BASE + 7)
+    ctx = vo.Context(375, 1242, 1)
+    k_gpu, d_gpu = ctx.sift(L)
+    k_ref, d_ref = oracle.sift(L)
+    assert len(k_ref) > 1000
+    _same_kps(k_gpu, k_ref)
+    assert np.array_equal(d_gpu, d_ref)
+
+
+def test_sift_match_batch_bit_exact(vo, oracle, syn):
+    import torch
+    B = 3
+    L, R = syn.independent_pairs(B)
+    ctx = vo.Context(375, 1242, B)
+    dl = torch.from_numpy(L).cuda()
+    dr = torch.from_numpy(R).cuda()
+    torch.cuda.synchronize()
+    stats = ctx.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), B)
+    for f in range(B):
+        kl, dl_ = ctx.fetch_keypoints(2 * f)
+        kr, dr_ = ctx.fetch_keypoints(2 * f + 1)
+        rkl, rdl = oracle.sift(L[f])
+        rkr, rdr = oracle.sift(R[f])
+        _same_kps(kl, rkl)
+        _same_kps(kr, rkr)
+        assert np.array_equal(dl_, rdl) and np.array_equal(dr_, rdr)
+        pairs = ctx.fetch_stereo_pairs(f)
+        ref = oracle.match(rdl, rdr)
+        assert stats[f][2] == len(ref)
+        assert np.array_equal(pairs, ref)
+
+
+def test_match_host_bit_exact(vo, oracle):
+    rng = np.random.default_rng(3)
+    base = rng.integers(0, 120, (700, 128)).astype(np.uint8)
+    F1 = base[:500].copy()
+    F2 = np.clip(base[100:].astype(int) + rng.integers(-3, 4, (600, 128)), 0, 255).astype(np.uint8)
+    F2[7] = F2[8]                       # exact duplicate -> ratio test edge
+    ctx = vo.Context(375, 1242, 1)
+    got = ctx.match(F1, F2)
+    ref = oracle.match(F1, F2)
+    assert len(ref) > 100
+    assert np.array_equal(got, ref)
