@@ -1,0 +1,156 @@
+#!/usr/bin/env python3
+"""bench.py — stereo frames/s of the VO hot path on MI355X.
+
+Workload (BASELINE.json configs[1]): SIFT detect+describe of both images +
+stereo matchFeatures, on 1242x375 synthetic stereo pairs (~2k keypoints per
+image), via libvo.so (hand-written HIP, gfx950).  One step = one batch of
+`--batch` independent stereo frames already resident in HBM.  With --gpus N
+(torchrun, one process per GPU, RCCL) each rank processes its own frames: weak
+scaling, no data-path collective; value = all frames / max-over-ranks time.
+
+Prints ONE JSON line (rank 0) with the driver's contract fields plus
+`roofline` (dominant kernel, HIP-event durations measured in this process)
+and `cpu_baseline` (the CPU oracle on a bounded sample, rank 0 at N=1).
+`--full` additionally times the full per-frame path (vo_step_batch).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "oracle"))   # cpu_baseline leg only
+
+import numpy as np  # noqa: E402
+
+ROWS, COLS = 375, 1242
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16, help="stereo frames per step")
+    ap.add_argument("--cpu-frames", type=int, default=3, help="frames in the CPU-oracle baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=3)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import vo_amd  # noqa: F401
+    from r7020e_visual_odometry_amd import vo, synthetic as syn, roofline
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    B = args.batch
+    # synthetic pairs: rank r renders frames [r*B, (r+1)*B) (seed 0x5EED0000 + frame)
+    L, R = syn.independent_pairs(B, ROWS, COLS, first=rank * B)
+    d_l = torch.from_numpy(L).to(f"cuda:{local}")
+    d_r = torch.from_numpy(R).to(f"cuda:{local}")
+    torch.cuda.synchronize()
+
+    ctx = vo.Context(ROWS, COLS, B, device=local)
+    stats = ctx.sift_match_batch_dev(d_l.data_ptr(), d_r.data_ptr(), B, stats=True)
+    for _ in range(args.warmup):
+        ctx.sift_match_batch_dev(d_l.data_ptr(), d_r.data_ptr(), B, stats=False)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.sift_match_batch_dev(d_l.data_ptr(), d_r.data_ptr(), B, stats=False)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    if dist is not None:
+        t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    frames = B * args.steps * world
+    fps = frames / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # ---- per-kernel HIP-event durations on libvo's stream (separate pass) ----
+    ctx.set_profiling(True)
+    for _ in range(args.profile_steps):
+        ctx.sift_match_batch_dev(d_l.data_ptr(), d_r.data_ptr(), B, stats=True)
+    kt = ctx.kernel_times()
+    ctx.set_profiling(False)
+    model = roofline.kernel_bytes(ROWS, COLS, 2 * B)
+    dom = max(kt.items(), key=lambda kv: kv[1][0])
+    dom_name, (dom_ms, dom_calls) = dom
+    avg_ms = dom_ms / dom_calls
+    roof = {"kernel": dom_name, "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
+            "avg_launch_us": avg_ms * 1e3}
+    if dom_name in model:
+        per_call_bytes, launches = model[dom_name]
+        per_launch = per_call_bytes / launches
+        achieved = per_launch / (avg_ms * 1e-3) / 1e9
+        roof.update({"achieved": achieved, "frac": achieved / HBM_PEAK_GBS, "bytes_per_launch": per_launch})
+    else:
+        roof.update({"achieved": None, "frac": None, "bytes_per_launch": None})
+    # whole-pyramid figure (SURVEY §8(d) per-frame model over the pyramid kernels' time)
+    pyr_names = [n for n in kt if n.startswith(("k_base_h", "k_blur_h", "k_blur_v", "k_down"))]
+    pyr_ms = sum(kt[n][0] for n in pyr_names) / args.profile_steps
+    pyr_bytes = 2 * B * roofline.pyramid_bytes_per_image(ROWS, COLS)
+    roof["pyramid_model_gbs"] = pyr_bytes / (pyr_ms * 1e-3) / 1e9 if pyr_ms > 0 else None
+    roof["kernel_ms_per_step"] = {n: round(v[0] / args.profile_steps, 4) for n, v in sorted(kt.items(), key=lambda kv: -kv[1][0])}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        import oracle
+        oracle.build()
+        n = args.cpu_frames
+        t0 = time.perf_counter()
+        for f in range(n):
+            oracle.sift_match_pair(L[f % B], R[f % B])
+        dt = time.perf_counter() - t0
+        cpu = {"value": n / dt, "unit": "stereo frames/s", "cores": 1, "kind": "port",
+               "sample": f"{n} synthetic 1242x375 stereo pairs (first {n} of the GPU batch), SIFT x2 + stereo match, "
+                         f"oracle/liboracle.so single-threaded, {dt:.1f} s"}
+
+    if rank == 0:
+        kp = np.mean([s[0] + s[1] for s in stats]) / 2
+        st = np.mean([s[2] for s in stats])
+        line = {
+            "metric": "stereo frames/sec @1242x375 (SIFT detect+describe x2 + stereo matchFeatures)",
+            "value": fps, "unit": "stereo frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32 (i8 MFMA for exact descriptor dot products)", "data": "synthetic",
+            "config": {"workload": "BASELINE configs[1]: SIFT detect+describe + BF match on 1242x375 synthetic stereo, "
+                                   "~2k keypoints/image", "frames_per_step_per_gpu": B, "rows": ROWS, "cols": COLS,
+                       "mean_keypoints_per_image": float(kp), "mean_stereo_matches": float(st),
+                       "parallelism": f"frames sharded over {world} GPU(s)"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,57 @@
+"""Algorithmic byte model of the hot-path kernels.
+
+SURVEY §8(d) prices the SIFT scale space as a materialised fp32 pyramid in
+which every Gaussian and DoG level is written once and read once:
+    B_img = W*H + 4 * (2*G + 2*D),  G = 6P, D = 5P,  P = sum of octave pixels.
+The per-kernel figures below split that model by the role each launch plays
+(bytes a kernel must move given its inputs and outputs, each touched once).
+They feed bench.py's `roofline.achieved` = bytes per launch / average launch
+duration of the dominant kernel.
+"""
+from __future__ import annotations
+
+import math
+
+
+def octave_dims(rows: int, cols: int, upsample: bool = True) -> list[tuple[int, int]]:
+    R, C = (rows * 2, cols * 2) if upsample else (rows, cols)
+    n = int(round(math.log2(min(R, C)) - 2)) + (1 if upsample else 0)
+    dims = []
+    for o in range(n):
+        if o:
+            R //= 2
+            C //= 2
+        dims.append((R, C))
+    return dims
+
+
+def pyramid_bytes_per_image(rows: int, cols: int, layers: int = 3) -> int:
+    """SURVEY §8(d) model for one image (u8 read + fp32 G/D written+read once)."""
+    P = sum(r * c for r, c in octave_dims(rows, cols))
+    G, D = (layers + 3) * P, (layers + 2) * P
+    return rows * cols + 4 * (2 * G + 2 * D)
+
+
+def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3) -> dict:
+    """Algorithmic bytes per CALL (all launches of that kernel name in one
+    batch of n_img images) and launches per call, per kernel name."""
+    dims = octave_dims(rows, cols)
+    lv = layers + 2          # blurred levels per octave (1..L+2)
+    out = {}
+
+    def add(name, nbytes, launches):
+        b, l = out.get(name, (0, 0))
+        out[name] = (b + nbytes, l + launches)
+
+    R0, C0 = dims[0]
+    add("k_base_h<true>", n_img * (rows * cols + 4 * R0 * C0), 1)        # u8 in, fp32 row pass out
+    add("k_blur_v<false>", n_img * 8 * R0 * C0, 1)                        # row pass in, G0 out
+    for o, (R, C) in enumerate(dims):
+        px = R * C * n_img
+        if o:
+            add("k_down", 8 * px, 1)                                      # 1 of 4 source px in, G0 out
+        add("k_blur_h", 8 * px * lv, lv)                                  # G_{i-1} in, row pass out
+        add("k_blur_v<true>", 16 * px * lv, lv)                           # row pass + G_{i-1} in, G_i + D_{i-1} out
+    # extremum test reads the L+2 DoG levels of every octave once
+    add("k_ext_mask", sum(4 * (layers + 2) * r * c for r, c in dims) * n_img, 1)
+    return out
