@@ -1,4 +1,21 @@
-// geom.hip — tracking + geometry stages (see vo_geom.h).
+// geom.hip — tracking + geometry stages of the per-frame path (see vo_geom.h).
+//
+//   find_remaining_points (VO.m:280-334)  four match jobs per frame whose row
+//       sets are index lists; k_compose turns each step's (i, j) pairs into the
+//       next step's lists, so no descriptor is ever copied.
+//   triangulate (VO.m:113-116)            k_gather_tri: one lane per tracked
+//       point, linear DLT + one-sided Jacobi SVD in f64 (oracle dlt_point).
+//   estworldpose (VO.m:123-127)           k_msac_hyp: one lane per hypothesis
+//       slot (Philox sample, Grunert P3P, 4th-point disambiguation);
+//       k_msac_score: one wave per hypothesis (lane-strided partial MSAC sums +
+//       fixed shuffle tree); k_msac_select: the sequential adaptive-termination
+//       loop replayed on the precomputed slots (one lane per frame);
+//       k_msac_final: inlier mask + camera pose.
+//   landmarks (VO.m:145-160, CreateLandmarksFromFeatures.m)  k_lm_filter
+//       (any-x-or-y equality test, quirk Q3) + block compaction, k_lm_tri (odd
+//       rows, z gates).  The world transform needs the chained pose and runs
+//       on the host after the 4x4 chain.
+// Float/double expressions mirror oracle/vo_ref.c operation for operation.
 #include "vo_geom.h"
 #include <cstring>
 
@@ -21,27 +38,771 @@ hipError_t geom_alloc(GeomBuffers& g, int max_frames, int kp_cap, int n_hyp)
     GA(g.inliers, F * K);
     GA(g.hyp, sizeof(MsacHyp) * F * n_hyp);
     GA(g.fg, sizeof(FrameGeom) * F);
+    GA(g.spos, sizeof(float) * F * K * 4);
+    GA(g.s_n, sizeof(int) * F);
     GA(g.lm_new, sizeof(int) * F * K);
     GA(g.lm_M, sizeof(int) * F);
     GA(g.lm_X, sizeof(float) * F * K * 3);
     GA(g.lm_keep, F * K);
     GA(g.lm_rows, sizeof(int) * F);
 #undef GA
-    return hipSuccess;
+    e = hipMemset(g.step_n, 0, sizeof(int) * 4 * F);
+    if (e != hipSuccess) return e;
+    return hipMemset(g.list_n, 0, sizeof(int) * 4 * F);
 }
 
 void geom_free(GeomBuffers& g)
 {
     hipFree(g.lists); hipFree(g.list_n); hipFree(g.step_i); hipFree(g.step_j); hipFree(g.step_n); hipFree(g.world);
-    hipFree(g.imgpt); hipFree(g.oldpos); hipFree(g.inliers); hipFree(g.hyp); hipFree(g.fg); hipFree(g.lm_new);
-    hipFree(g.lm_M); hipFree(g.lm_X); hipFree(g.lm_keep); hipFree(g.lm_rows);
+    hipFree(g.imgpt); hipFree(g.oldpos); hipFree(g.inliers); hipFree(g.hyp); hipFree(g.fg); hipFree(g.spos);
+    hipFree(g.s_n); hipFree(g.lm_new); hipFree(g.lm_M); hipFree(g.lm_X); hipFree(g.lm_keep); hipFree(g.lm_rows);
     g = GeomBuffers();
 }
 
-void geom_fill_track_jobs(const GeomBuffers& g, MatchJob* jobs, int max_frames, int first, const SiftBuffers& sb,
+static inline int* glist(const GeomBuffers& g, int f, int l) { return g.lists + ((size_t)f * TL_COUNT + l) * g.kp_cap; }
+
+void geom_fill_track_jobs(const GeomBuffers& g, MatchJob* jobs, int M, int first, const SiftBuffers& sb,
                           int* pair_i, int* pair_j, int* pair_n, int kp_cap)
 {
-    (void)g; (void)jobs; (void)max_frames; (void)first; (void)sb; (void)pair_i; (void)pair_j; (void)pair_n; (void)kp_cap;
+    const size_t ds = (size_t)kp_cap * VO_DESC_LEN;
+    auto D = [&](int slot) { return (const uint8_t*)(sb.desc + slot * ds); };
+    auto Mt = [&](int slot) { return (const DescMeta*)(sb.meta + (size_t)slot * kp_cap); };
+    for (int f = 0; f < M; ++f) {
+        const int cl = 2 * f, cr = 2 * f + 1;
+        const int pl = f ? 2 * (f - 1) : 2 * M, pr = pl + 1;
+        const int pp = f ? f - 1 : M;
+        for (int s = 0; s < 4; ++s) {
+            MatchJob& J = jobs[first + s * M + f];
+            memset(&J, 0, sizeof(J));
+            J.out_i = g.step_i + ((size_t)s * M + f) * kp_cap;
+            J.out_j = g.step_j + ((size_t)s * M + f) * kp_cap;
+            J.out_n = g.step_n + s * M + f;
+            J.cap = kp_cap;
+        }
+        // step 0: lm = matchFeatures(cur.l_desc, old.l_desc)            VO.m:283
+        MatchJob& J0 = jobs[first + 0 * M + f];
+        J0.d1 = D(cl); J0.m1 = Mt(cl); J0.idx1 = nullptr; J0.n1 = sb.n_kp + cl;
+        J0.d2 = D(pl); J0.m2 = Mt(pl); J0.idx2 = pair_i + (size_t)pp * kp_cap; J0.n2 = pair_n + pp;
+        // step 1: rm = matchFeatures(cur.r_desc, old.r_desc)            VO.m:293
+        MatchJob& J1 = jobs[first + 1 * M + f];
+        J1.d1 = D(cr); J1.m1 = Mt(cr); J1.idx1 = nullptr; J1.n1 = sb.n_kp + cr;
+        J1.d2 = D(pr); J1.m2 = Mt(pr); J1.idx2 = glist(g, f, TL_OR1); J1.n2 = g.list_n + 4 * f + 0;
+        // step 2: cm = matchFeatures(cur.l_desc, cur.r_desc)            VO.m:311
+        MatchJob& J2 = jobs[first + 2 * M + f];
+        J2.d1 = D(cl); J2.m1 = Mt(cl); J2.idx1 = glist(g, f, TL_CL); J2.n1 = g.list_n + 4 * f + 0;
+        J2.d2 = D(cr); J2.m2 = Mt(cr); J2.idx2 = glist(g, f, TL_CR); J2.n2 = g.list_n + 4 * f + 1;
+        // step 3: last = matchFeatures(cur.l_desc, old.l_desc)          VO.m:323
+        MatchJob& J3 = jobs[first + 3 * M + f];
+        J3.d1 = D(cl); J3.m1 = Mt(cl); J3.idx1 = glist(g, f, TL_CL2); J3.n1 = g.list_n + 4 * f + 2;
+        J3.d2 = D(pl); J3.m2 = Mt(pl); J3.idx2 = glist(g, f, TL_OL2); J3.n2 = g.list_n + 4 * f + 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// index composition after each tracking step (VO.m:287-290,297-300,305-308,
+// 314-317,326-333).  grid (blocks, B)
+// ---------------------------------------------------------------------------
+struct ComposeArgs {
+    int* lists; int* list_n; const int* step_i; const int* step_j; const int* step_n;
+    const int* pair_i; const int* pair_j; const int* pair_n;
+    int M, kp_cap, step;
+};
+
+__global__ void k_compose(ComposeArgs a)
+{
+    const int f = blockIdx.y, K = a.kp_cap, M = a.M;
+    const int s = a.step;
+    int n = a.step_n[s * M + f];
+    if (n > K) n = K;
+    if (n < 0) n = 0;
+    const int* si = a.step_i + ((size_t)s * M + f) * K;
+    const int* sj = a.step_j + ((size_t)s * M + f) * K;
+    int* L = a.lists + (size_t)f * TL_COUNT * K;
+    const int pp = f ? f - 1 : M;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const int i = si[k], j = sj[k];
+        if (s == 0) {
+            L[TL_OL1 * K + k] = a.pair_i[(size_t)pp * K + j];
+            L[TL_OR1 * K + k] = a.pair_j[(size_t)pp * K + j];
+            L[TL_CL * K + k] = i;
+        } else if (s == 1) {
+            L[TL_OL2 * K + k] = L[TL_OL1 * K + j];
+            L[TL_OR2 * K + k] = L[TL_OR1 * K + j];
+            L[TL_CR * K + k] = i;
+        } else if (s == 2) {
+            L[TL_CL2 * K + k] = L[TL_CL * K + i];
+            L[TL_CR2 * K + k] = L[TL_CR * K + j];
+        } else {
+            L[TL_OLF * K + k] = L[TL_OL2 * K + j];
+            L[TL_ORF * K + k] = L[TL_OR2 * K + j];
+            L[TL_CLF * K + k] = L[TL_CL2 * K + i];
+            L[TL_CRF * K + k] = L[TL_CR2 * K + i];
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.list_n[4 * f + s] = n;
+}
+
+// ---------------------------------------------------------------------------
+// DLT triangulation (oracle dlt_point)
+// ---------------------------------------------------------------------------
+__device__ void dlt_point_dev(float u1f, float v1f, float u2f, float v2f, const double* P1, const double* P2, double X[3])
+{
+    double u1 = u1f, v1 = v1f, u2 = u2f, v2 = v2f;
+    double A[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        A[0][c] = u1 * P1[8 + c] - P1[c];
+        A[1][c] = v1 * P1[8 + c] - P1[4 + c];
+        A[2][c] = u2 * P2[8 + c] - P2[c];
+        A[3][c] = v2 * P2[8 + c] - P2[4 + c];
+    }
+    double V[4][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}};
+    for (int sweep = 0; sweep < 30; ++sweep) {
+        int rotated = 0;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int q = p + 1; q < 4; ++q) {
+                double al = 0, be = 0, ga = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    al = al + A[i][p] * A[i][p];
+                    be = be + A[i][q] * A[i][q];
+                    ga = ga + A[i][p] * A[i][q];
+                }
+                if (ga == 0.0 || fabs(ga) <= 1e-15 * sqrt(al * be)) continue;
+                rotated = 1;
+                double zeta = (be - al) / (2.0 * ga);
+                double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                double c = 1.0 / sqrt(1.0 + t * t);
+                double s = c * t;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    double ap = A[i][p], aq = A[i][q];
+                    A[i][p] = c * ap - s * aq;
+                    A[i][q] = s * ap + c * aq;
+                    double vp = V[i][p], vq = V[i][q];
+                    V[i][p] = c * vp - s * vq;
+                    V[i][q] = s * vp + c * vq;
+                }
+            }
+        if (!rotated) break;
+    }
+    int jmin = 0;
+    double nmin = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        double nj = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) nj = nj + A[i][j] * A[i][j];
+        if (j == 0 || nj < nmin) { nmin = nj; jmin = j; }
+    }
+    double v0 = 0, v1_ = 0, v2_ = 0, w = 1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (j == jmin) { v0 = V[0][j]; v1_ = V[1][j]; v2_ = V[2][j]; w = V[3][j]; }
+    X[0] = (double)(float)(v0 / w);
+    X[1] = (double)(float)(v1_ / w);
+    X[2] = (double)(float)(v2_ / w);
+}
+
+struct CalibDev { double P1[12], P2[12], K[9]; };
+
+// gather tracked positions and triangulate the old stereo pair. grid (blocks, B)
+__global__ void k_gather_tri(const vo_keypoint* __restrict__ kp, int kp_cap, const int* __restrict__ lists,
+                             const int* __restrict__ list_n, float* __restrict__ oldpos, double* __restrict__ imgpt,
+                             double* __restrict__ world, int M, CalibDev cal)
+{
+    const int f = blockIdx.y, K = kp_cap;
+    int n = list_n[4 * f + 3];
+    const int cl = 2 * f;
+    const int pl = f ? 2 * (f - 1) : 2 * M, pr = pl + 1;
+    const int* L = lists + (size_t)f * TL_COUNT * K;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const vo_keypoint ol = kp[(size_t)pl * K + L[TL_OLF * K + k]];
+        const vo_keypoint orr = kp[(size_t)pr * K + L[TL_ORF * K + k]];
+        const vo_keypoint cu = kp[(size_t)cl * K + L[TL_CLF * K + k]];
+        float* op = oldpos + ((size_t)f * K + k) * 4;
+        op[0] = ol.x; op[1] = ol.y; op[2] = orr.x; op[3] = orr.y;
+        double* ip = imgpt + ((size_t)f * K + k) * 2;
+        ip[0] = cu.x; ip[1] = cu.y;
+        double X[3];
+        dlt_point_dev(ol.x, ol.y, orr.x, orr.y, cal.P1, cal.P2, X);
+        double* w = world + ((size_t)f * K + k) * 3;
+        w[0] = X[0]; w[1] = X[1]; w[2] = X[2];
+    }
+}
+
+// standalone triangulation of position quads (x1, y1, x2, y2)
+__global__ void k_tri_list(const float* __restrict__ pos, int n, CalibDev cal, double* __restrict__ X)
+{
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        double Y[3];
+        dlt_point_dev(pos[4 * k], pos[4 * k + 1], pos[4 * k + 2], pos[4 * k + 3], cal.P1, cal.P2, Y);
+        X[3 * k] = Y[0]; X[3 * k + 1] = Y[1]; X[3 * k + 2] = Y[2];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// P3P (oracle_p3p) — Grunert's quartic by polynomial algebra, deterministic
+// bracketing/bisection root finder (template recursion = the oracle's).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double peval_dev(const double* a, int deg, double x)
+{
+    double r = a[deg];
+    for (int i = deg - 1; i >= 0; --i) r = r * x + a[i];
+    return r;
+}
+
+template <int MAXDEG>
+__device__ int real_roots_dev(const double* a_in, int deg, double* roots);
+
+template <>
+__device__ int real_roots_dev<1>(const double*, int, double*) { return 0; }
+
+template <int MAXDEG>
+__device__ int real_roots_dev(const double* a_in, int deg, double* roots)
+{
+    double a[5];
+    for (int i = 0; i <= deg; ++i) a[i] = a_in[i];
+    double amax = 0;
+    for (int i = 0; i <= deg; ++i) if (fabs(a[i]) > amax) amax = fabs(a[i]);
+    if (amax == 0.0) return 0;
+    while (deg > 0 && fabs(a[deg]) <= 1e-14 * amax) deg--;
+    if (deg == 0) return 0;
+    if (deg == 1) { roots[0] = -a[0] / a[1]; return 1; }
+    if (deg == 2) {
+        double disc = a[1] * a[1] - 4.0 * a[2] * a[0];
+        if (disc < 0) return 0;
+        double sq = sqrt(disc);
+        double q = -0.5 * (a[1] + (a[1] >= 0 ? sq : -sq));
+        double r1 = q / a[2], r2 = (q != 0.0) ? a[0] / q : r1;
+        if (r1 <= r2) { roots[0] = r1; roots[1] = r2; } else { roots[0] = r2; roots[1] = r1; }
+        return 2;
+    }
+    double d[4] = {0, 0, 0, 0};
+    for (int i = 1; i <= deg; ++i) d[i - 1] = a[i] * (double)i;
+    double crit[4];
+    int nc = real_roots_dev<MAXDEG - 1>(d, deg - 1, crit);
+    double B = 0;
+    for (int i = 0; i < deg; ++i) { double t = fabs(a[i] / a[deg]); if (t > B) B = t; }
+    B = B + 1.0;
+    double pts[6];
+    int np = 0;
+    pts[np++] = -B;
+    for (int i = 0; i < nc; ++i) if (crit[i] > -B && crit[i] < B) pts[np++] = crit[i];
+    pts[np++] = B;
+    int nr = 0;
+    for (int k = 0; k + 1 < np; ++k) {
+        double lo = pts[k], hi = pts[k + 1];
+        double flo = peval_dev(a, deg, lo), fhi = peval_dev(a, deg, hi);
+        if (flo == 0.0) { if (nr == 0 || roots[nr - 1] != lo) roots[nr++] = lo; continue; }
+        if ((flo < 0) == (fhi < 0)) continue;
+        for (int it = 0; it < 200; ++it) {
+            double mid = 0.5 * (lo + hi);
+            if (mid <= lo || mid >= hi) break;
+            double fm = peval_dev(a, deg, mid);
+            if (fm == 0.0) { lo = hi = mid; break; }
+            if ((fm < 0) == (flo < 0)) { lo = mid; flo = fm; } else hi = mid;
+        }
+        roots[nr++] = 0.5 * (lo + hi);
+    }
+    return nr;
+}
+
+__device__ __forceinline__ void pmul_dev(const double* a, int da, const double* b, int db, double* out)
+{
+    for (int i = 0; i <= da + db; ++i) out[i] = 0.0;
+    for (int i = 0; i <= da; ++i)
+        for (int j = 0; j <= db; ++j) out[i + j] = out[i + j] + a[i] * b[j];
+}
+
+__device__ __forceinline__ void bearing_dev(const double* K, double u, double v, double f[3])
+{
+    double yn = (v - K[5]) / K[4];
+    double xn = (u - K[2] - K[1] * yn) / K[0];
+    double n = sqrt(xn * xn + yn * yn + 1.0);
+    f[0] = xn / n; f[1] = yn / n; f[2] = 1.0 / n;
+}
+
+__device__ __forceinline__ void cross3_dev(const double* a, const double* b, double* c)
+{
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+__device__ __forceinline__ int normalize3_dev(double* a)
+{
+    double n = sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+    if (!(n > 0)) return 0;
+    a[0] = a[0] / n; a[1] = a[1] / n; a[2] = a[2] / n;
+    return 1;
+}
+
+__device__ int align3_dev(const double Pw[3][3], const double Pc[3][3], double R[9], double t[3])
+{
+    double ew[3][3], ec[3][3];
+    double d1[3], d2[3];
+    for (int i = 0; i < 3; ++i) { ew[0][i] = Pw[1][i] - Pw[0][i]; d1[i] = Pw[2][i] - Pw[0][i]; }
+    if (!normalize3_dev(ew[0])) return 0;
+    cross3_dev(ew[0], d1, ew[2]);
+    if (!normalize3_dev(ew[2])) return 0;
+    cross3_dev(ew[2], ew[0], ew[1]);
+    for (int i = 0; i < 3; ++i) { ec[0][i] = Pc[1][i] - Pc[0][i]; d2[i] = Pc[2][i] - Pc[0][i]; }
+    if (!normalize3_dev(ec[0])) return 0;
+    cross3_dev(ec[0], d2, ec[2]);
+    if (!normalize3_dev(ec[2])) return 0;
+    cross3_dev(ec[2], ec[0], ec[1]);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R[3 * i + j] = ec[0][i] * ew[0][j] + ec[1][i] * ew[1][j] + ec[2][i] * ew[2][j];
+    double mw[3], mc[3];
+    for (int i = 0; i < 3; ++i) {
+        mw[i] = (Pw[0][i] + Pw[1][i] + Pw[2][i]) / 3.0;
+        mc[i] = (Pc[0][i] + Pc[1][i] + Pc[2][i]) / 3.0;
+    }
+    for (int i = 0; i < 3; ++i) t[i] = mc[i] - (R[3 * i] * mw[0] + R[3 * i + 1] * mw[1] + R[3 * i + 2] * mw[2]);
+    return 1;
+}
+
+__device__ __forceinline__ double reproj_err2_dev(const double R[9], const double t[3], const double* K, const double* X,
+                                                  const double* uv)
+{
+    double xc = R[0] * X[0] + R[1] * X[1] + R[2] * X[2] + t[0];
+    double yc = R[3] * X[0] + R[4] * X[1] + R[5] * X[2] + t[1];
+    double zc = R[6] * X[0] + R[7] * X[1] + R[8] * X[2] + t[2];
+    if (!(zc > 0)) return INFINITY;
+    double xn = xc / zc, yn = yc / zc;
+    double u = K[0] * xn + K[1] * yn + K[2];
+    double v = K[4] * yn + K[5];
+    double du = u - uv[0], dv = v - uv[1];
+    return du * du + dv * dv;
+}
+
+// one P3P + 4th-point selection; returns 1 if valid
+__device__ int p3p_hyp_dev(const double im3[3][2], const double w3[3][3], const double* w4, const double* im4,
+                           const double* K, double Rb[9], double tb[3])
+{
+    double j[3][3];
+    for (int i = 0; i < 3; ++i) bearing_dev(K, im3[i][0], im3[i][1], j[i]);
+    double dv[3];
+    for (int i = 0; i < 3; ++i) dv[i] = w3[1][i] - w3[2][i];
+    double a2 = dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2];
+    for (int i = 0; i < 3; ++i) dv[i] = w3[0][i] - w3[2][i];
+    double b2 = dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2];
+    for (int i = 0; i < 3; ++i) dv[i] = w3[0][i] - w3[1][i];
+    double c2 = dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2];
+    if (!(a2 > 0 && b2 > 0 && c2 > 0)) return 0;
+    double ca = j[1][0] * j[2][0] + j[1][1] * j[2][1] + j[1][2] * j[2][2];
+    double cb = j[0][0] * j[2][0] + j[0][1] * j[2][1] + j[0][2] * j[2][2];
+    double cg = j[0][0] * j[1][0] + j[0][1] * j[1][1] + j[0][2] * j[1][2];
+    double Kq = (a2 - c2) / b2, cb2 = c2 / b2;
+    double N[3] = {1.0 + Kq, -2.0 * Kq * cb, Kq - 1.0};
+    double D[2] = {2.0 * cg, -2.0 * ca};
+    double Q[3] = {1.0, -2.0 * cb, 1.0};
+    double DD[3], NN[5], ND[4], QDD[5];
+    pmul_dev(D, 1, D, 1, DD);
+    pmul_dev(N, 2, N, 2, NN);
+    pmul_dev(N, 2, D, 1, ND);
+    pmul_dev(Q, 2, DD, 2, QDD);
+    double P[5];
+    for (int i = 0; i < 5; ++i) {
+        double v = NN[i] - cb2 * QDD[i];
+        if (i < 3) v = v + DD[i];
+        if (i < 4) v = v - 2.0 * cg * ND[i];
+        P[i] = v;
+    }
+    double roots[4];
+    int nr = real_roots_dev<4>(P, 4, roots);
+    int ns = 0, best = -1;
+    double be = INFINITY;
+    for (int k = 0; k < nr; ++k) {
+        double v = roots[k];
+        if (!(v > 0)) continue;
+        double Dv = D[0] + D[1] * v;
+        if (Dv == 0.0) continue;
+        double u = (N[0] + N[1] * v + N[2] * v * v) / Dv;
+        if (!(u > 0)) continue;
+        double Qv = Q[0] + Q[1] * v + Q[2] * v * v;
+        if (!(Qv > 0)) continue;
+        double s1 = sqrt(b2 / Qv), s2 = u * s1, s3 = v * s1;
+        double Pc[3][3];
+        for (int i = 0; i < 3; ++i) { Pc[0][i] = s1 * j[0][i]; Pc[1][i] = s2 * j[1][i]; Pc[2][i] = s3 * j[2][i]; }
+        double R[9], t[3];
+        if (align3_dev(w3, Pc, R, t)) {
+            double e = reproj_err2_dev(R, t, K, w4, im4);
+            if (e < be) {
+                be = e; best = ns;
+                for (int q = 0; q < 9; ++q) Rb[q] = R[q];
+                for (int q = 0; q < 3; ++q) tb[q] = t[q];
+            }
+            ns++;
+        }
+        if (ns == 4) break;
+    }
+    return best >= 0;
+}
+
+struct MsacArgs {
+    const double* img; const double* world; const int* n; int n_stride;   // n[f * n_stride]
+    MsacHyp* hyp; FrameGeom* fg; uint8_t* inliers;
+    int kp_cap, n_hyp, max_trials;
+    double thr, conf;
+    uint32_t seed;
+    uint32_t key0;           // frame key of frame 0 (frame f uses key0 + f)
+    double K[9];
+};
+
+__device__ __forceinline__ int msac_n(const MsacArgs& a, int f)
+{
+    int n = a.n[(size_t)f * a.n_stride];
+    return n < 0 ? 0 : (n > a.kp_cap ? a.kp_cap : n);
+}
+
+// one lane per (frame, slot).  grid (ceil(n_hyp/64), B)
+__global__ __launch_bounds__(64) void k_msac_hyp(MsacArgs a)
+{
+    const int f = blockIdx.y;
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.n_hyp) return;
+    MsacHyp* h = a.hyp + (size_t)f * a.n_hyp + s;
+    const int n = msac_n(a, f);
+    h->valid = 0;
+    if (n < 4 || s >= a.max_trials) return;
+    const double* img = a.img + (size_t)f * a.kp_cap * 2;
+    const double* world = a.world + (size_t)f * a.kp_cap * 3;
+    uint32_t idx[4];
+    bool ok = false;
+    for (uint32_t att = 0; att < 16 && !ok; ++att) {
+        vo_u32x4 c = {{(uint32_t)s, att, a.key0 + (uint32_t)f, 0x5EEDu}};
+        vo_u32x4 r = vo_philox4x32_10(c, a.seed, 0x9E3779B9u);
+        for (int q = 0; q < 4; ++q) idx[q] = vo_rand_index(r.v[q], (uint32_t)n);
+        ok = idx[0] != idx[1] && idx[0] != idx[2] && idx[0] != idx[3] && idx[1] != idx[2] && idx[1] != idx[3] &&
+             idx[2] != idx[3];
+    }
+    if (!ok) return;
+    double im3[3][2], w3[3][3];
+    for (int q = 0; q < 3; ++q) {
+        im3[q][0] = img[2 * idx[q]]; im3[q][1] = img[2 * idx[q] + 1];
+        for (int i = 0; i < 3; ++i) w3[q][i] = world[3 * idx[q] + i];
+    }
+    double R[9], t[3];
+    if (!p3p_hyp_dev(im3, w3, world + 3 * idx[3], img + 2 * idx[3], a.K, R, t)) return;
+    for (int q = 0; q < 9; ++q) h->R[q] = R[q];
+    for (int q = 0; q < 3; ++q) h->t[q] = t[q];
+    h->valid = 1;
+}
+
+// one wave per (frame, slot): MSAC score = 64 lane-strided partials + tree
+__global__ __launch_bounds__(256) void k_msac_score(MsacArgs a, int B)
+{
+    const int lane = threadIdx.x & 63;
+    const long total = (long)B * a.n_hyp;
+    for (long t = (long)blockIdx.x * 4 + (threadIdx.x >> 6); t < total; t += (long)gridDim.x * 4) {
+        const int f = (int)(t / a.n_hyp), s = (int)(t - (long)f * a.n_hyp);
+        MsacHyp* h = a.hyp + (size_t)f * a.n_hyp + s;
+        if (!h->valid) continue;
+        const int n = msac_n(a, f);
+        const double* img = a.img + (size_t)f * a.kp_cap * 2;
+        const double* world = a.world + (size_t)f * a.kp_cap * 3;
+        double R[9], tt[3];
+        for (int q = 0; q < 9; ++q) R[q] = h->R[q];
+        for (int q = 0; q < 3; ++q) tt[q] = h->t[q];
+        double part = 0.0;
+        int cnt = 0;
+        for (int k = lane; k < n; k += 64) {
+            double e = reproj_err2_dev(R, tt, a.K, world + 3 * k, img + 2 * k);
+            if (e < a.thr) cnt++;
+            part = part + (e < a.thr ? e : a.thr);
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            part = part + __shfl_down(part, off);
+            cnt += __shfl_xor(cnt, off);
+        }
+        if (lane == 0) { h->score = part; h->n_in = cnt; }
+    }
+}
+
+__device__ int msac_trials_needed_dev(int n_in, int n, double conf)
+{
+    double w = (double)n_in / (double)n;
+    double w4 = w * w * w * w;
+    if (!(w4 > 1e-300)) return 0x7fffffff;
+    double den = vo_log_d(1.0 - w4);
+    if (!(den < 0)) return 1;
+    double num = vo_log_d(1.0 - conf);
+    double N = ceil(num / den);
+    if (N > 2147483647.0) return 0x7fffffff;
+    if (N < 1.0) return 1;
+    return (int)N;
+}
+
+// sequential MSAC replay (adaptive trial count) + final inliers/pose.  block 64 per frame
+__global__ __launch_bounds__(64) void k_msac_select(MsacArgs a)
+{
+    __shared__ int s_best;
+    __shared__ int s_status;
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const int n = msac_n(a, f);
+    FrameGeom* g = a.fg + f;
+    if (lane == 0) {
+        int status = VO_OK, best = -1;
+        if (n < 4) status = VO_ERR_TOO_FEW_POINTS;
+        else {
+            int num_trials = a.max_trials, trials = 0, best_in = 0;
+            double best_score = INFINITY;
+            for (int s = 0; s < a.max_trials && s < a.n_hyp && trials < num_trials; ++s) {
+                const MsacHyp* h = a.hyp + (size_t)f * a.n_hyp + s;
+                if (!h->valid) continue;
+                trials++;
+                if (h->score < best_score) {
+                    best_score = h->score; best = s; best_in = h->n_in;
+                    int need = msac_trials_needed_dev(h->n_in, n, a.conf);
+                    if (need < num_trials) num_trials = need;
+                }
+            }
+            if (best < 0 || best_in < 4) status = VO_ERR_NO_CONSENSUS;
+        }
+        s_best = best;
+        s_status = status;
+        g->status = status;
+        g->best = best;
+        g->n_tracked = n;
+    }
+    __syncthreads();
+    const int best = s_best;
+    if (s_status != VO_OK) {
+        if (lane == 0) {
+            g->n_inliers = 0;
+            for (int q = 0; q < 16; ++q) g->T[q] = (q % 5 == 0) ? 1.0 : 0.0;
+        }
+        return;
+    }
+    const MsacHyp* h = a.hyp + (size_t)f * a.n_hyp + best;
+    double R[9], t[3];
+    for (int q = 0; q < 9; ++q) R[q] = h->R[q];
+    for (int q = 0; q < 3; ++q) t[q] = h->t[q];
+    const double* img = a.img + (size_t)f * a.kp_cap * 2;
+    const double* world = a.world + (size_t)f * a.kp_cap * 3;
+    int cnt = 0;
+    for (int k = lane; k < n; k += 64) {
+        const int in = reproj_err2_dev(R, t, a.K, world + 3 * k, img + 2 * k) < a.thr;
+        a.inliers[(size_t)f * a.kp_cap + k] = (uint8_t)in;
+        cnt += in;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+    if (lane == 0) {
+        g->n_inliers = cnt;
+        for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 3; ++j) g->T[4 * i + j] = R[3 * j + i];
+            g->T[4 * i + 3] = -(R[i] * t[0] + R[3 + i] * t[1] + R[6 + i] * t[2]);
+        }
+        g->T[12] = 0; g->T[13] = 0; g->T[14] = 0; g->T[15] = 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// landmarks
+// ---------------------------------------------------------------------------
+// stereo subset positions of frame f (VO.m:141-142): spos[f][j] = (lx, ly, rx, ry)
+__global__ void k_stereo_pos(const vo_keypoint* __restrict__ kp, int kp_cap, const int* __restrict__ pair_i,
+                             const int* __restrict__ pair_j, const int* __restrict__ pair_n, float* __restrict__ spos,
+                             int* __restrict__ s_n)
+{
+    const int f = blockIdx.y, K = kp_cap;
+    int n = pair_n[f];
+    if (n > K) n = K;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        const vo_keypoint l = kp[(size_t)(2 * f) * K + pair_i[(size_t)f * K + j]];
+        const vo_keypoint r = kp[(size_t)(2 * f + 1) * K + pair_j[(size_t)f * K + j]];
+        float* p = spos + ((size_t)f * K + j) * 4;
+        p[0] = l.x; p[1] = l.y; p[2] = r.x; p[3] = r.y;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) s_n[f] = n;
+}
+
+__device__ __forceinline__ uint32_t block_exscan_1024_g(uint32_t v, uint32_t* sh, uint32_t* total)
+{
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        uint32_t s = lane < 16 ? sh[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            uint32_t y = __shfl_up(s, o);
+            if (lane >= o) s += y;
+        }
+        if (lane < 16) sh[16 + lane] = s;
+    }
+    __syncthreads();
+    uint32_t before = wid ? sh[16 + wid - 1] : 0;
+    *total = sh[16 + 15];
+    __syncthreads();
+    return before + x - v;
+}
+
+// new-landmark filter (VO.m:147-154) + compaction.  one block (1024) per frame.
+// old positions: oldpos[f][k] (x1, y1, x2, y2) for k < *kn (kn[f * kn_stride]).
+// flags: per-frame byte scratch (lm_keep, rewritten later by k_lm_tri).
+__global__ __launch_bounds__(1024) void k_lm_filter(const float* __restrict__ spos, const int* __restrict__ s_n,
+                                                    const float* __restrict__ oldpos, const int* __restrict__ kn,
+                                                    int kn_stride, int kp_cap, uint8_t* __restrict__ flags,
+                                                    int* __restrict__ lm_new, int* __restrict__ lm_M,
+                                                    int* __restrict__ lm_rows)
+{
+    __shared__ uint32_t sh[32];
+    const int f = blockIdx.x, tid = threadIdx.x, K = kp_cap;
+    int S = s_n[f];
+    if (S > K) S = K;
+    int nk = kn[(size_t)f * kn_stride];
+    if (nk > K) nk = K;
+    if (nk < 0) nk = 0;
+    const float* sp = spos + (size_t)f * K * 4;
+    const float* op = oldpos + (size_t)f * K * 4;
+    uint8_t* fl = flags + (size_t)f * K;
+    const int chunk = (S + 1023) / 1024;
+    const int a0 = tid * chunk, e = min(a0 + chunk, S);
+    uint32_t cnt = 0;
+    for (int j = a0; j < e; ++j) {
+        const float lx = sp[4 * j], ly = sp[4 * j + 1], rx = sp[4 * j + 2], ry = sp[4 * j + 3];
+        bool hit = false;
+        for (int k = 0; k < nk && !hit; ++k)
+            if (op[4 * k] == lx || op[4 * k + 1] == ly) hit = true;
+        for (int k = 0; k < nk && !hit; ++k)
+            if (op[4 * k + 2] == rx || op[4 * k + 3] == ry) hit = true;
+        fl[j] = hit ? 0 : 1;
+        cnt += hit ? 0 : 1;
+    }
+    uint32_t total;
+    uint32_t base = block_exscan_1024_g(cnt, sh, &total);
+    for (int j = a0; j < e; ++j)
+        if (fl[j]) lm_new[(size_t)f * K + base++] = j;
+    __syncthreads();
+    if (tid == 0) {
+        lm_M[f] = (int)total;
+        lm_rows[f] = 2;                                     // zeros(size(features_l,2),3): 2 rows
+        for (int m = (int)total; m < 2; ++m) fl[m] = 0;     // rows beyond M stay zero rows
+    }
+}
+
+// CreateLandmarksFromFeatures: odd 1-based rows (even 0-based), triangulate, z gates.
+__global__ void k_lm_tri(const float* __restrict__ spos, const int* __restrict__ lm_new, const int* __restrict__ lm_M,
+                         int kp_cap, CalibDev cal, float* __restrict__ lm_X, uint8_t* __restrict__ lm_keep,
+                         int* __restrict__ lm_rows)
+{
+    const int f = blockIdx.y, K = kp_cap;
+    const int M = lm_M[f];
+    for (int m = blockIdx.x * blockDim.x + threadIdx.x; m < M; m += gridDim.x * blockDim.x) {
+        uint8_t keep = 0;
+        if ((m & 1) == 0) {
+            const int j = lm_new[(size_t)f * K + m];
+            const float* p = spos + ((size_t)f * K + j) * 4;
+            double X[3];
+            dlt_point_dev(p[0], p[1], p[2], p[3], cal.P1, cal.P2, X);
+            keep = !(X[2] < 0) && !(X[2] > 80);
+            float* o = lm_X + ((size_t)f * K + m) * 3;
+            o[0] = (float)X[0]; o[1] = (float)X[1]; o[2] = (float)X[2];
+            if (keep) atomicMax(lm_rows + f, m + 1);
+        }
+        lm_keep[(size_t)f * K + m] = keep;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host enqueue
+// ---------------------------------------------------------------------------
+static CalibDev calib_dev(const vo_calib& c)
+{
+    CalibDev d;
+    memcpy(d.P1, c.P1, sizeof(d.P1));
+    memcpy(d.P2, c.P2, sizeof(d.P2));
+    memcpy(d.K, c.K, sizeof(d.K));
+    return d;
+}
+
+static MsacArgs msac_args(GeomBuffers& g, const double* img, const double* world, const int* n, int n_stride,
+                          const double K[9], const vo_ransac_params& rp, uint32_t key0)
+{
+    MsacArgs a;
+    a.img = img; a.world = world; a.n = n; a.n_stride = n_stride;
+    a.hyp = g.hyp; a.fg = g.fg; a.inliers = g.inliers;
+    a.kp_cap = g.kp_cap; a.n_hyp = g.n_hyp; a.max_trials = rp.max_num_trials < g.n_hyp ? rp.max_num_trials : g.n_hyp;
+    a.thr = rp.max_reprojection_error * rp.max_reprojection_error;
+    a.conf = rp.confidence / 100.0;
+    a.seed = rp.seed;
+    a.key0 = key0;
+    memcpy(a.K, K, sizeof(a.K));
+    return a;
+}
+
+static void msac_enqueue(const MsacArgs& a, int B, hipStream_t s)
+{
+    VO_LAUNCH(k_msac_hyp, dim3((a.n_hyp + 63) / 64, B), dim3(64), 0, s, a);
+    int blocks = (B * a.n_hyp + 3) / 4;
+    if (blocks > 4096) blocks = 4096;
+    VO_LAUNCH(k_msac_score, dim3(blocks), dim3(256), 0, s, a, B);
+    VO_LAUNCH(k_msac_select, dim3(B), dim3(64), 0, s, a);
+}
+
+void track_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_track_jobs, const StepArgs& a,
+                   const vo_match_params& mp, hipStream_t s)
+{
+    const int B = a.B, M = a.max_frames, K = a.kp_cap;
+    ComposeArgs ca;
+    ca.lists = g.lists; ca.list_n = g.list_n; ca.step_i = g.step_i; ca.step_j = g.step_j; ca.step_n = g.step_n;
+    ca.pair_i = a.pair_i; ca.pair_j = a.pair_j; ca.pair_n = a.pair_n; ca.M = M; ca.kp_cap = K;
+    for (int step = 0; step < 4; ++step) {
+        match_launch(mb, d_track_jobs + step * M, B, mp, s);
+        ca.step = step;
+        VO_LAUNCH(k_compose, dim3(16, B), dim3(256), 0, s, ca);
+    }
+}
+
+void geom_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_track_jobs, const StepArgs& a,
+                  const vo_match_params& mp, hipStream_t s)
+{
+    const int B = a.B, M = a.max_frames, K = a.kp_cap;
+    track_enqueue(g, mb, d_track_jobs, a, mp, s);
+    CalibDev cal = calib_dev(a.calib);
+    VO_LAUNCH(k_gather_tri, dim3(16, B), dim3(64), 0, s, a.sb->kp, K, g.lists, g.list_n, g.oldpos, g.imgpt, g.world, M, cal);
+    MsacArgs ma = msac_args(g, g.imgpt, g.world, g.list_n + 3, 4, a.calib.K, a.rp, (uint32_t)a.frame_index0);
+    msac_enqueue(ma, B, s);
+    VO_LAUNCH(k_stereo_pos, dim3(16, B), dim3(256), 0, s, a.sb->kp, K, a.pair_i, a.pair_j, a.pair_n, g.spos, g.s_n);
+    VO_LAUNCH(k_lm_filter, dim3(B), dim3(1024), 0, s, g.spos, g.s_n, g.oldpos, g.list_n + 3, 4, K, g.lm_keep, g.lm_new,
+              g.lm_M, g.lm_rows);
+    VO_LAUNCH(k_lm_tri, dim3(16, B), dim3(64), 0, s, g.spos, g.lm_new, g.lm_M, K, cal, g.lm_X, g.lm_keep, g.lm_rows);
+}
+
+void triangulate_launch(const float* pos, int n, const vo_calib& c, double* X, hipStream_t s)
+{
+    if (n <= 0) return;
+    int blocks = (n + 63) / 64;
+    if (blocks > 1024) blocks = 1024;
+    VO_LAUNCH(k_tri_list, dim3(blocks), dim3(64), 0, s, pos, n, calib_dev(c), X);
+}
+
+void estworldpose_launch(GeomBuffers& g, const double* img, const double* world, const int* n, const double K[9],
+                         const vo_ransac_params& rp, uint32_t frame_key, hipStream_t s)
+{
+    MsacArgs ma = msac_args(g, img, world, n, 0, K, rp, frame_key);
+    msac_enqueue(ma, 1, s);
+}
+
+void landmarks_launch(GeomBuffers& g, const int* kn, const vo_calib& c, hipStream_t s)
+{
+    CalibDev cal = calib_dev(c);
+    VO_LAUNCH(k_lm_filter, dim3(1), dim3(1024), 0, s, g.spos, g.s_n, g.oldpos, kn, 0, g.kp_cap, g.lm_keep, g.lm_new, g.lm_M,
+              g.lm_rows);
+    VO_LAUNCH(k_lm_tri, dim3(16, 1), dim3(64), 0, s, g.spos, g.lm_new, g.lm_M, g.kp_cap, cal, g.lm_X, g.lm_keep, g.lm_rows);
 }
 
 }  // namespace vo

@@ -392,20 +392,322 @@ int vo_fetch_stereo_pairs(vo_ctx* c, int frame, uint32_t* pairs, int capacity, i
 
 }  // extern "C"
 
-// ---- stage-2 entry points (tracking / geometry / loop) --------------------
-extern "C" {
-int vo_track(vo_ctx* c, const uint8_t*, const uint8_t*, int, const uint8_t*, int, const uint8_t*, int, uint32_t*, int, int*)
-{ return fail(c, VO_ERR_STATE, "vo_track: not built yet"); }
-int vo_triangulate(vo_ctx* c, const float*, const float*, int, const double*, const double*, double*)
-{ return fail(c, VO_ERR_STATE, "vo_triangulate: not built yet"); }
-int vo_estworldpose(vo_ctx* c, const double*, const double*, int, const double*, const vo_ransac_params*, uint32_t, double*,
-                    uint8_t*, int*)
-{ return fail(c, VO_ERR_STATE, "vo_estworldpose: not built yet"); }
-int vo_landmarks(vo_ctx* c, const float*, const float*, int, const float*, const float*, int, const double*, double*, int, int*)
-{ return fail(c, VO_ERR_STATE, "vo_landmarks: not built yet"); }
-int vo_step(vo_ctx* c, const uint8_t*, const uint8_t*, int, vo_step_out*) { return fail(c, VO_ERR_STATE, "vo_step: not built yet"); }
-int vo_step_batch(vo_ctx* c, const uint8_t*, const uint8_t*, int, int, vo_step_out*) { return fail(c, VO_ERR_STATE, "not built yet"); }
-int vo_step_batch_dev(vo_ctx* c, const uint8_t*, const uint8_t*, int, vo_step_out*) { return fail(c, VO_ERR_STATE, "not built yet"); }
-int vo_get_landmarks(vo_ctx* c, double*, int, int*) { return fail(c, VO_ERR_STATE, "not built yet"); }
-int vo_reset(vo_ctx* c) { return fail(c, VO_ERR_STATE, "not built yet"); }
+// ---- tracking / geometry / loop --------------------------------------------
+static vo_calib calib_of(const double P1[12], const double P2[12], const double* K)
+{
+    vo_calib c;
+    memcpy(c.P1, P1, sizeof(c.P1));
+    memcpy(c.P2, P2, sizeof(c.P2));
+    if (K) memcpy(c.K, K, sizeof(c.K));
+    else for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) c.K[3 * i + j] = P1[4 * i + j];
+    return c;
 }
+
+static StepArgs step_args(vo_ctx* c, int B)
+{
+    StepArgs a;
+    a.sb = &c->sb;
+    a.pair_i = c->d_pair_i; a.pair_j = c->d_pair_j; a.pair_n = c->d_pair_n;
+    a.max_frames = c->max_batch; a.B = B; a.kp_cap = c->sb.kp_cap;
+    a.first_has_prev = c->have_features ? 1 : 0;
+    a.frame_index0 = c->frame_index;
+    a.calib = c->calib;
+    a.rp = c->rp;
+    return a;
+}
+
+static void mat4_mul(const double* A, const double* B, double* C)
+{
+    double T[16];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            T[4 * i + j] = A[4 * i] * B[j] + A[4 * i + 1] * B[4 + j] + A[4 * i + 2] * B[8 + j] + A[4 * i + 3] * B[12 + j];
+    memcpy(C, T, sizeof(T));
+}
+
+// world transform of one landmark row, rounded through single (CreateLandmarksFromFeatures.m:17)
+static void lm_world(const double* pose, const float* X, double* out)
+{
+    const double x0 = X[0], x1 = X[1], x2 = X[2];
+    for (int a = 0; a < 3; ++a) {
+        double w = pose[4 * a] * x0 + pose[4 * a + 1] * x1 + pose[4 * a + 2] * x2 + pose[4 * a + 3];
+        out[a] = (double)(float)w;
+    }
+}
+
+// copy frame f's SIFT results + stereo pairs into the carry slots (prev of the next call's frame 0)
+static int enqueue_carry(vo_ctx* c, int f)
+{
+    const int M = c->max_batch, K = c->sb.kp_cap;
+    for (int side = 0; side < 2; ++side) {
+        const int src = 2 * f + side, dst = 2 * M + side;
+        HIPC(c, hipMemcpyAsync(c->sb.kp + (size_t)dst * K, c->sb.kp + (size_t)src * K, sizeof(vo_keypoint) * K,
+                               hipMemcpyDeviceToDevice, c->stream));
+        HIPC(c, hipMemcpyAsync(c->sb.desc + (size_t)dst * K * VO_DESC_LEN, c->sb.desc + (size_t)src * K * VO_DESC_LEN,
+                               (size_t)K * VO_DESC_LEN, hipMemcpyDeviceToDevice, c->stream));
+        HIPC(c, hipMemcpyAsync(c->sb.meta + (size_t)dst * K, c->sb.meta + (size_t)src * K, sizeof(DescMeta) * K,
+                               hipMemcpyDeviceToDevice, c->stream));
+        HIPC(c, hipMemcpyAsync(c->sb.n_kp + dst, c->sb.n_kp + src, sizeof(int), hipMemcpyDeviceToDevice, c->stream));
+    }
+    HIPC(c, hipMemcpyAsync(c->d_pair_i + (size_t)M * K, c->d_pair_i + (size_t)f * K, sizeof(int) * K, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->d_pair_j + (size_t)M * K, c->d_pair_j + (size_t)f * K, sizeof(int) * K, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->d_pair_n + M, c->d_pair_n + f, sizeof(int), hipMemcpyDeviceToDevice, c->stream));
+    return VO_OK;
+}
+
+// The VO.m loop body for B frames whose images are in device memory.
+static int run_batch(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B, vo_step_out* outs)
+{
+    if (!c->has_calib) return fail(c, VO_ERR_STATE, "vo_step: no calibration (vo_set_calib)");
+    const int K = c->sb.kp_cap;
+    enqueue_sift_stereo(c, d_l, d_r, B);
+    StepArgs a = step_args(c, B);
+    geom_enqueue(c->gb, c->mb, c->d_jobs + job_track(c, 0, 0), a, c->mp, c->stream);
+    std::vector<FrameGeom> fg(B);
+    std::vector<int> nkp(2 * B), np(B), rows(B);
+    HIPC(c, hipMemcpyAsync(fg.data(), c->gb.fg, sizeof(FrameGeom) * B, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(nkp.data(), c->sb.n_kp, sizeof(int) * 2 * B, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(np.data(), c->d_pair_n, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(rows.data(), c->gb.lm_rows, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
+    int rc = enqueue_carry(c, B - 1);
+    if (rc) return rc;
+    rc = finish(c);
+    if (rc) return rc;
+    std::vector<std::vector<float>> X(B);
+    std::vector<std::vector<uint8_t>> keep(B);
+    for (int f = 0; f < B; ++f) {
+        int r = std::min(rows[f], K);
+        X[f].resize((size_t)r * 3);
+        keep[f].resize(r);
+        if (r > 0) {
+            HIPC(c, hipMemcpyAsync(X[f].data(), c->gb.lm_X + (size_t)f * K * 3, sizeof(float) * 3 * r, hipMemcpyDeviceToHost, c->stream));
+            HIPC(c, hipMemcpyAsync(keep[f].data(), c->gb.lm_keep + (size_t)f * K, r, hipMemcpyDeviceToHost, c->stream));
+        }
+    }
+    HIPC(c, hipStreamSynchronize(c->stream));
+    for (int f = 0; f < B; ++f) {
+        vo_step_out& o = outs[f];
+        memset(&o, 0, sizeof(o));
+        o.n_left = nkp[2 * f]; o.n_right = nkp[2 * f + 1]; o.n_stereo = np[f];
+        memcpy(o.rel_pose, I4, sizeof(I4));
+        const bool tracked = f > 0 || c->have_features;
+        if (tracked) {
+            o.status = fg[f].status;
+            o.n_tracked = fg[f].n_tracked;
+            o.n_inliers = fg[f].n_inliers;
+            if (o.status == VO_OK) {
+                memcpy(o.rel_pose, fg[f].T, sizeof(fg[f].T));
+                mat4_mul(c->pose, fg[f].T, c->pose);
+            }
+            const int r = (int)keep[f].size();
+            o.n_landmarks = r;
+            size_t base = c->landmarks.size();
+            c->landmarks.resize(base + (size_t)r * 3, 0.0);
+            for (int m = 0; m < r; ++m)
+                if (keep[f][m]) lm_world(c->pose, &X[f][(size_t)m * 3], &c->landmarks[base + (size_t)m * 3]);
+        }
+        memcpy(o.pose, c->pose, sizeof(c->pose));
+    }
+    c->have_features = true;
+    c->frame_index += B;
+    return VO_OK;
+}
+
+extern "C" {
+
+int vo_step_batch_dev(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B, vo_step_out* outs)
+{
+    if (!c || !d_l || !d_r || !outs || B < 1 || B > c->max_batch) return fail(c, VO_ERR_ARG, "vo_step_batch_dev: bad arguments");
+    begin_call(c);
+    int rc = run_batch(c, d_l, d_r, B, outs);
+    g_prof = nullptr;
+    return rc;
+}
+
+int vo_step_batch(vo_ctx* c, const uint8_t* lefts, const uint8_t* rights, int ld, int B, vo_step_out* outs)
+{
+    if (!c || !lefts || !rights || !outs || B < 1 || B > c->max_batch || ld < c->cols)
+        return fail(c, VO_ERR_ARG, "vo_step_batch: bad arguments");
+    begin_call(c);
+    const size_t fs = (size_t)c->rows * c->cols;
+    uint8_t* dl = c->d_img;
+    uint8_t* dr = c->d_img + fs * B;
+    HIPC(c, hipMemcpy2DAsync(dl, c->cols, lefts, ld, c->cols, (size_t)c->rows * B, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpy2DAsync(dr, c->cols, rights, ld, c->cols, (size_t)c->rows * B, hipMemcpyHostToDevice, c->stream));
+    int rc = run_batch(c, dl, dr, B, outs);
+    g_prof = nullptr;
+    return rc;
+}
+
+int vo_step(vo_ctx* c, const uint8_t* left, const uint8_t* right, int ld, vo_step_out* out)
+{
+    return vo_step_batch(c, left, right, ld, 1, out);
+}
+
+int vo_get_landmarks(vo_ctx* c, double* out, int capacity, int* rows)
+{
+    if (!c) return VO_ERR_ARG;
+    int r = (int)(c->landmarks.size() / 3);
+    if (rows) *rows = r;
+    if (out) memcpy(out, c->landmarks.data(), sizeof(double) * 3 * std::min(r, capacity));
+    return r > capacity && out ? fail(c, VO_ERR_CAPACITY, "vo_get_landmarks: %d rows exceed capacity %d", r, capacity) : VO_OK;
+}
+
+int vo_reset(vo_ctx* c)
+{
+    if (!c) return VO_ERR_ARG;
+    hipSetDevice(c->device);
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->have_features = false;
+    c->frame_index = 0;
+    memcpy(c->pose, I4, sizeof(I4));
+    c->landmarks.clear();
+    HIPC(c, hipMemset(c->d_pair_n + c->max_batch, 0, sizeof(int)));
+    return VO_OK;
+}
+
+// Standalone calls use frame slot 0 and the carry slots: they invalidate the
+// loop state of vo_step (call vo_reset before stepping again).
+static int upload_desc(vo_ctx* c, int slot, const uint8_t* d, int n)
+{
+    const int K = c->sb.kp_cap;
+    if (n) HIPC(c, hipMemcpyAsync(c->sb.desc + (size_t)slot * K * VO_DESC_LEN, d, (size_t)n * VO_DESC_LEN, hipMemcpyHostToDevice, c->stream));
+    desc_meta_launch(c->sb.desc + (size_t)slot * K * VO_DESC_LEN, c->sb.meta + (size_t)slot * K, n, c->stream);
+    HIPC(c, hipMemcpyAsync(c->sb.n_kp + slot, &n, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));   // &n is a stack value
+    return VO_OK;
+}
+
+int vo_track(vo_ctx* c, const uint8_t* old_l, const uint8_t* old_r, int n_old, const uint8_t* cur_l, int n_cl,
+             const uint8_t* cur_r, int n_cr, uint32_t* idx_out, int capacity, int* K_out)
+{
+    if (!c || n_old < 0 || n_cl < 0 || n_cr < 0) return fail(c, VO_ERR_ARG, "vo_track: bad arguments");
+    const int K = c->sb.kp_cap, M = c->max_batch;
+    if (n_old > K || n_cl > K || n_cr > K) return fail(c, VO_ERR_CAPACITY, "vo_track: more rows than max_keypoints");
+    begin_call(c);
+    c->have_features = false;
+    int rc;
+    if ((rc = upload_desc(c, 2 * M, old_l, n_old))) return rc;
+    if ((rc = upload_desc(c, 2 * M + 1, old_r, n_old))) return rc;
+    if ((rc = upload_desc(c, 0, cur_l, n_cl))) return rc;
+    if ((rc = upload_desc(c, 1, cur_r, n_cr))) return rc;
+    std::vector<int> iota(std::max(n_old, 1));
+    for (int k = 0; k < n_old; ++k) iota[k] = k;
+    if (n_old) {
+        HIPC(c, hipMemcpy(c->d_pair_i + (size_t)M * K, iota.data(), sizeof(int) * n_old, hipMemcpyHostToDevice));
+        HIPC(c, hipMemcpy(c->d_pair_j + (size_t)M * K, iota.data(), sizeof(int) * n_old, hipMemcpyHostToDevice));
+    }
+    HIPC(c, hipMemcpy(c->d_pair_n + M, &n_old, sizeof(int), hipMemcpyHostToDevice));
+    StepArgs a = step_args(c, 1);
+    track_enqueue(c->gb, c->mb, c->d_jobs + job_track(c, 0, 0), a, c->mp, c->stream);
+    int n = 0;
+    HIPC(c, hipMemcpyAsync(&n, c->gb.list_n + 3, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    rc = finish(c);
+    if (rc) return rc;
+    if (K_out) *K_out = n;
+    const int m = std::min(n, capacity);
+    if (m > 0 && idx_out) {
+        std::vector<int> ol(m), cl(m), cr(m);
+        HIPC(c, hipMemcpy(ol.data(), track_list(c->gb, 0, TL_OLF), sizeof(int) * m, hipMemcpyDeviceToHost));
+        HIPC(c, hipMemcpy(cl.data(), track_list(c->gb, 0, TL_CLF), sizeof(int) * m, hipMemcpyDeviceToHost));
+        HIPC(c, hipMemcpy(cr.data(), track_list(c->gb, 0, TL_CRF), sizeof(int) * m, hipMemcpyDeviceToHost));
+        for (int k = 0; k < m; ++k) {
+            idx_out[3 * k] = (uint32_t)ol[k] + 1;
+            idx_out[3 * k + 1] = (uint32_t)cl[k] + 1;
+            idx_out[3 * k + 2] = (uint32_t)cr[k] + 1;
+        }
+    }
+    if (n > capacity) return fail(c, VO_ERR_CAPACITY, "vo_track: %d rows exceed capacity %d", n, capacity);
+    return VO_OK;
+}
+
+int vo_triangulate(vo_ctx* c, const float* x1, const float* x2, int n, const double P1[12], const double P2[12], double* X)
+{
+    if (!c || n < 0 || (n && (!x1 || !x2 || !X)) || !P1 || !P2) return fail(c, VO_ERR_ARG, "vo_triangulate: bad arguments");
+    begin_call(c);
+    const vo_calib cal = calib_of(P1, P2, nullptr);
+    const int K = c->sb.kp_cap;
+    std::vector<float> q((size_t)std::min(n, K) * 4 + 4);
+    for (int b = 0; b < n; b += K) {
+        const int m = std::min(K, n - b);
+        for (int k = 0; k < m; ++k) {
+            q[4 * k] = x1[2 * (b + k)]; q[4 * k + 1] = x1[2 * (b + k) + 1];
+            q[4 * k + 2] = x2[2 * (b + k)]; q[4 * k + 3] = x2[2 * (b + k) + 1];
+        }
+        HIPC(c, hipMemcpyAsync(c->gb.oldpos, q.data(), sizeof(float) * 4 * m, hipMemcpyHostToDevice, c->stream));
+        triangulate_launch(c->gb.oldpos, m, cal, c->gb.world, c->stream);
+        HIPC(c, hipMemcpyAsync(X + 3 * (size_t)b, c->gb.world, sizeof(double) * 3 * m, hipMemcpyDeviceToHost, c->stream));
+        int rc = finish(c);
+        if (rc) return rc;
+        g_prof = c->prof.on ? &c->prof : nullptr;
+    }
+    g_prof = nullptr;
+    return VO_OK;
+}
+
+int vo_estworldpose(vo_ctx* c, const double* img, const double* world, int n, const double K9[9],
+                    const vo_ransac_params* params, uint32_t frame_key, double T[16], uint8_t* inliers, int* n_inliers)
+{
+    if (!c || n < 0 || (n && (!img || !world)) || !K9 || !T) return fail(c, VO_ERR_ARG, "vo_estworldpose: bad arguments");
+    if (n > c->sb.kp_cap) return fail(c, VO_ERR_CAPACITY, "vo_estworldpose: %d points exceed max_keypoints", n);
+    const vo_ransac_params rp = params ? *params : c->rp;
+    if (rp.max_num_trials > c->gb.n_hyp) return fail(c, VO_ERR_ARG, "vo_estworldpose: max_num_trials > context's");
+    if (n_inliers) *n_inliers = 0;
+    if (n < 4) return fail(c, VO_ERR_TOO_FEW_POINTS, "estworldpose: need at least 4 points, got %d", n);
+    begin_call(c);
+    c->have_features = false;
+    HIPC(c, hipMemcpyAsync(c->gb.imgpt, img, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->gb.world, world, sizeof(double) * 3 * n, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->d_fn, &n, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    estworldpose_launch(c->gb, c->gb.imgpt, c->gb.world, c->d_fn, K9, rp, frame_key, c->stream);
+    FrameGeom g;
+    HIPC(c, hipMemcpyAsync(&g, c->gb.fg, sizeof(g), hipMemcpyDeviceToHost, c->stream));
+    if (inliers) HIPC(c, hipMemcpyAsync(inliers, c->gb.inliers, n, hipMemcpyDeviceToHost, c->stream));
+    int rc = finish(c);
+    if (rc) return rc;
+    memcpy(T, g.T, sizeof(g.T));
+    if (n_inliers) *n_inliers = g.n_inliers;
+    if (g.status == VO_ERR_NO_CONSENSUS) return fail(c, g.status, "estworldpose: no consensus (MSAC found no model with >= 4 inliers)");
+    if (g.status != VO_OK) return fail(c, g.status, "estworldpose failed (%d)", g.status);
+    return VO_OK;
+}
+
+int vo_landmarks(vo_ctx* c, const float* l_pos, const float* r_pos, int S, const float* old_l, const float* old_r, int Kn,
+                 const double pose[16], double* out, int capacity, int* rows_out)
+{
+    if (!c || S < 0 || Kn < 0 || !pose || (S && (!l_pos || !r_pos)) || (Kn && (!old_l || !old_r)))
+        return fail(c, VO_ERR_ARG, "vo_landmarks: bad arguments");
+    if (!c->has_calib) return fail(c, VO_ERR_STATE, "vo_landmarks: no calibration");
+    const int K = c->sb.kp_cap;
+    if (S > K || Kn > K) return fail(c, VO_ERR_CAPACITY, "vo_landmarks: more rows than max_keypoints");
+    begin_call(c);
+    c->have_features = false;
+    std::vector<float> sp((size_t)S * 4 + 4), op((size_t)Kn * 4 + 4);
+    for (int j = 0; j < S; ++j) { sp[4 * j] = l_pos[2 * j]; sp[4 * j + 1] = l_pos[2 * j + 1]; sp[4 * j + 2] = r_pos[2 * j]; sp[4 * j + 3] = r_pos[2 * j + 1]; }
+    for (int k = 0; k < Kn; ++k) { op[4 * k] = old_l[2 * k]; op[4 * k + 1] = old_l[2 * k + 1]; op[4 * k + 2] = old_r[2 * k]; op[4 * k + 3] = old_r[2 * k + 1]; }
+    int cnt[2] = {S, Kn};
+    HIPC(c, hipMemcpyAsync(c->gb.spos, sp.data(), sizeof(float) * 4 * S, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->gb.oldpos, op.data(), sizeof(float) * 4 * Kn, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->gb.s_n, &cnt[0], sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->d_fn, &cnt[1], sizeof(int), hipMemcpyHostToDevice, c->stream));
+    landmarks_launch(c->gb, c->d_fn, c->calib, c->stream);
+    int rows = 0;
+    HIPC(c, hipMemcpyAsync(&rows, c->gb.lm_rows, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    int rc = finish(c);
+    if (rc) return rc;
+    std::vector<float> X((size_t)rows * 3);
+    std::vector<uint8_t> keep(rows);
+    HIPC(c, hipMemcpy(X.data(), c->gb.lm_X, sizeof(float) * 3 * rows, hipMemcpyDeviceToHost));
+    HIPC(c, hipMemcpy(keep.data(), c->gb.lm_keep, rows, hipMemcpyDeviceToHost));
+    if (rows_out) *rows_out = rows;
+    if (out) {
+        for (int m = 0; m < rows && m < capacity; ++m) {
+            out[3 * m] = out[3 * m + 1] = out[3 * m + 2] = 0.0;
+            if (keep[m]) lm_world(pose, &X[(size_t)m * 3], out + 3 * m);
+        }
+    }
+    if (rows > capacity) return fail(c, VO_ERR_CAPACITY, "vo_landmarks: %d rows exceed capacity %d", rows, capacity);
+    return VO_OK;
+}
+
+}  // extern "C"

@@ -43,6 +43,8 @@ struct GeomBuffers {
     MsacHyp* hyp = nullptr;      // [max_frames][n_hyp]
     FrameGeom* fg = nullptr;     // [max_frames]
     // landmarks
+    float* spos = nullptr;       // [max_frames][kp_cap][4] stereo subset positions (lx, ly, rx, ry)
+    int* s_n = nullptr;          // [max_frames]
     int* lm_new = nullptr;       // [max_frames][kp_cap]  compacted indices of new stereo matches
     int* lm_M = nullptr;         // [max_frames]
     float* lm_X = nullptr;       // [max_frames][kp_cap][3] camera-frame points of odd rows
@@ -74,11 +76,18 @@ struct StepArgs {
 // landmark kernels for frames [0, B).  match jobs at d_jobs + first.
 void geom_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_track_jobs, const StepArgs& a,
                   const vo_match_params& mp, hipStream_t s);
+// tracking only (4 matches + compositions); lists/list_n valid afterwards.
+void track_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_track_jobs, const StepArgs& a,
+                   const vo_match_params& mp, hipStream_t s);
+static inline int* track_list(const GeomBuffers& g, int f, int l) { return g.lists + ((size_t)f * TL_COUNT + l) * g.kp_cap; }
 
-// Standalone launchers used by the single-call ABI functions.
-void triangulate_launch(const float* x1, const float* x2, int n, const double* P1, const double* P2, double* X,
-                        hipStream_t s);
+// Standalone launchers used by the single-call ABI functions (frame slot 0).
+// pos: [n][4] (x1, y1, x2, y2) device floats.
+void triangulate_launch(const float* pos, int n, const vo_calib& c, double* X, hipStream_t s);
 void estworldpose_launch(GeomBuffers& g, const double* img, const double* world, const int* n, const double K[9],
                          const vo_ransac_params& rp, uint32_t frame_key, hipStream_t s);
+// landmark filter + CreateLandmarksFromFeatures on g.spos/g.s_n (frame 0) vs
+// g.oldpos with *kn old rows.
+void landmarks_launch(GeomBuffers& g, const int* kn, const vo_calib& c, hipStream_t s);
 
 }  // namespace vo

@@ -260,6 +260,93 @@ class Context:
         self._check(self.lib.vo_fetch_stereo_pairs(self.h, frame, _p(pairs, C.c_uint32), cap, C.byref(n)))
         return pairs[: min(n.value, cap)].copy()
 
+    # ---- find_remaining_points ----
+    def track(self, old_l, old_r, cur_l, cur_r) -> np.ndarray:
+        """-> idx [K, 3] 1-based rows {old_row, cur_left_row, cur_right_row}."""
+        a = [np.ascontiguousarray(x, np.uint8).reshape(-1, 128) for x in (old_l, old_r, cur_l, cur_r)]
+        cap = max(x.shape[0] for x in a) + 1
+        idx = np.zeros((cap, 3), np.uint32)
+        n = C.c_int(0)
+        self._check(self.lib.vo_track(self.h, _p(a[0], C.c_uint8), _p(a[1], C.c_uint8), a[0].shape[0],
+                                      _p(a[2], C.c_uint8), a[2].shape[0], _p(a[3], C.c_uint8), a[3].shape[0],
+                                      _p(idx, C.c_uint32), cap, C.byref(n)))
+        return idx[: n.value].copy()
+
+    # ---- triangulate ----
+    def triangulate(self, x1, x2, P1, P2) -> np.ndarray:
+        x1 = np.ascontiguousarray(x1, np.float32).reshape(-1, 2)
+        x2 = np.ascontiguousarray(x2, np.float32).reshape(-1, 2)
+        P1 = np.ascontiguousarray(P1, np.float64)
+        P2 = np.ascontiguousarray(P2, np.float64)
+        X = np.zeros((x1.shape[0], 3))
+        self._check(self.lib.vo_triangulate(self.h, _p(x1, C.c_float), _p(x2, C.c_float), x1.shape[0],
+                                            _p(P1, C.c_double), _p(P2, C.c_double), _p(X, C.c_double)))
+        return X
+
+    # ---- estworldpose ----
+    def estworldpose(self, imagePoints, worldPoints, K, params: RansacParams | None = None, frame_key: int = 0,
+                     raise_on_failure: bool = True):
+        """-> (status, T 4x4 camera pose in world, inlier mask, n_inliers).  Like MATLAB,
+        raises on < 4 points / no consensus unless raise_on_failure=False."""
+        img = np.ascontiguousarray(imagePoints, np.float64).reshape(-1, 2)
+        world = np.ascontiguousarray(worldPoints, np.float64).reshape(-1, 3)
+        K = np.ascontiguousarray(K, np.float64)
+        T = np.zeros(16)
+        inl = np.zeros(max(img.shape[0], 1), np.uint8)
+        nin = C.c_int(0)
+        rc = self.lib.vo_estworldpose(self.h, _p(img, C.c_double), _p(world, C.c_double), img.shape[0], _p(K, C.c_double),
+                                      C.byref(params) if params else None, frame_key, _p(T, C.c_double),
+                                      _p(inl, C.c_uint8), C.byref(nin))
+        if raise_on_failure:
+            self._check(rc)
+        else:
+            self._check(rc, allow=(VO_ERR_TOO_FEW_POINTS, VO_ERR_NO_CONSENSUS))
+        return rc, T.reshape(4, 4), inl[: img.shape[0]].astype(bool), nin.value
+
+    # ---- new-landmark filter + CreateLandmarksFromFeatures ----
+    def landmarks(self, l_pos, r_pos, old_l, old_r, pose) -> np.ndarray:
+        a = [np.ascontiguousarray(x, np.float32).reshape(-1, 2) for x in (l_pos, r_pos, old_l, old_r)]
+        pose = np.ascontiguousarray(pose, np.float64)
+        cap = a[0].shape[0] + 2
+        out = np.zeros((cap, 3))
+        rows = C.c_int(0)
+        self._check(self.lib.vo_landmarks(self.h, _p(a[0], C.c_float), _p(a[1], C.c_float), a[0].shape[0],
+                                          _p(a[2], C.c_float), _p(a[3], C.c_float), a[2].shape[0],
+                                          _p(pose, C.c_double), _p(out, C.c_double), cap, C.byref(rows)))
+        return out[: rows.value].copy()
+
+    # ---- the VO.m loop body ----
+    def step_batch(self, lefts: np.ndarray, rights: np.ndarray) -> np.ndarray:
+        L = np.ascontiguousarray(lefts, np.uint8)
+        R = np.ascontiguousarray(rights, np.uint8)
+        B = L.shape[0]
+        outs = np.zeros(B, STEP_DTYPE)
+        self._check(self.lib.vo_step_batch(self.h, _p(L, C.c_uint8), _p(R, C.c_uint8), L.shape[2], B,
+                                           outs.ctypes.data_as(C.POINTER(StepOut))))
+        return outs
+
+    def step_batch_dev(self, d_lefts: int, d_rights: int, B: int) -> np.ndarray:
+        outs = np.zeros(B, STEP_DTYPE)
+        self._check(self.lib.vo_step_batch_dev(self.h, C.c_void_p(d_lefts), C.c_void_p(d_rights), B,
+                                               outs.ctypes.data_as(C.POINTER(StepOut))))
+        return outs
+
+    def step(self, left: np.ndarray, right: np.ndarray):
+        return self.step_batch(left[None], right[None])[0]
+
+    def get_landmarks(self) -> np.ndarray:
+        rows = C.c_int(0)
+        self._check(self.lib.vo_get_landmarks(self.h, None, 0, C.byref(rows)))
+        out = np.zeros((max(rows.value, 1), 3))
+        self._check(self.lib.vo_get_landmarks(self.h, _p(out, C.c_double), rows.value, C.byref(rows)))
+        return out[: rows.value].copy()
+
+    def reset(self):
+        self._check(self.lib.vo_reset(self.h))
+
+    def set_calib(self, calib: Calib):
+        self._check(self.lib.vo_set_calib(self.h, C.byref(calib)))
+
     # ---- profiling ----
     def set_profiling(self, on: bool):
         self._check(self.lib.vo_set_profiling(self.h, 1 if on else 0))
