@@ -199,6 +199,9 @@ int vo_step_batch_dev(vo_ctx* ctx, const uint8_t* d_lefts, const uint8_t* d_righ
 int vo_get_landmarks(vo_ctx* ctx, double* out, int capacity, int* rows);
 /* Reset loop state (features, pose, landmarks). */
 int vo_reset(vo_ctx* ctx);
+/* Global index of the next frame (the MSAC Philox key of frame i is
+ * seed, frame i); a rank that starts a sequence shard at frame k sets k here. */
+int vo_set_frame_index(vo_ctx* ctx, long frame_index);
 
 /* ---- benchmark workload: SIFT + stereo match on B independent pairs ---- */
 typedef struct {

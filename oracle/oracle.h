@@ -72,11 +72,17 @@ int oracle_landmarks(const float* l_pos, const float* r_pos, int S, const float*
                      const double pose[16], double* out, int capacity);
 
 /* Whole loop over a sequence (VO.m:64-232): frames [F][rows*cols] u8 tightly
- * packed.  outs[F]; landmarks appended to lm_out (capacity rows). Returns
- * landmark rows total. */
+ * packed.  outs[F]; landmarks appended to lm_out (capacity rows). Frame f uses
+ * MSAC key key0 + f (key0 = global index of frame 0).  Returns landmark rows. */
 long oracle_run_sequence(const uint8_t* lefts, const uint8_t* rights, int F, int rows, int cols,
                          const vo_calib* calib, const vo_sift_params* sp, const vo_match_params* mp,
-                         const vo_ransac_params* rp, vo_step_out* outs, double* lm_out, long lm_cap);
+                         const vo_ransac_params* rp, vo_step_out* outs, double* lm_out, long lm_cap,
+                         uint32_t key0);
+
+/* spec primitive evaluation for KATs (spec_eval.c) */
+void oracle_spec_eval(int fn, const double* in, double* out, int n);
+void oracle_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t* out);
+int oracle_gauss_radius(double sigma);
 
 /* SIFT + stereo match of one pair (bench workload, configs[1]). */
 int oracle_sift_match_pair(const uint8_t* left, const uint8_t* right, int rows, int cols,

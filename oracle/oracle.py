@@ -109,7 +109,13 @@ def lib():
         L.oracle_landmarks.argtypes = [P(C.c_float), P(C.c_float), C.c_int, P(C.c_float), P(C.c_float), C.c_int,
                                        P(C.c_double), P(C.c_double), P(C.c_double), P(C.c_double), C.c_int]
         L.oracle_run_sequence.argtypes = [P(C.c_uint8), P(C.c_uint8), C.c_int, C.c_int, C.c_int, P(Calib), P(SiftParams),
-                                          P(MatchParams), P(RansacParams), P(StepOut), P(C.c_double), C.c_long]
+                                          P(MatchParams), P(RansacParams), P(StepOut), P(C.c_double), C.c_long,
+                                          C.c_uint32]
+        L.oracle_spec_eval.argtypes = [C.c_int, P(C.c_double), P(C.c_double), C.c_int]
+        L.oracle_spec_eval.restype = None
+        L.oracle_philox.argtypes = [C.c_uint32] * 6 + [P(C.c_uint32)]
+        L.oracle_philox.restype = None
+        L.oracle_gauss_radius.argtypes = [C.c_double]
         L.oracle_run_sequence.restype = C.c_long
         L.oracle_sift_match_pair.argtypes = [P(C.c_uint8), P(C.c_uint8), C.c_int, C.c_int, P(SiftParams), P(MatchParams),
                                              P(C.c_int), P(C.c_int)]
@@ -237,7 +243,7 @@ STEP_DTYPE = np.dtype([("status", "<i4"), ("n_left", "<i4"), ("n_right", "<i4"),
                        ("rel_pose", "<f8", (4, 4)), ("pose", "<f8", (4, 4))])
 
 
-def run_sequence(L, R, P1, P2, sp=None, mp=None, rp=None, lm_cap: int = 1 << 20):
+def run_sequence(L, R, P1, P2, sp=None, mp=None, rp=None, lm_cap: int = 1 << 20, key0: int = 0):
     L = np.ascontiguousarray(L, np.uint8)
     R = np.ascontiguousarray(R, np.uint8)
     F, rows, cols = L.shape
@@ -247,7 +253,7 @@ def run_sequence(L, R, P1, P2, sp=None, mp=None, rp=None, lm_cap: int = 1 << 20)
     n = lib().oracle_run_sequence(_p(L, C.c_uint8), _p(R, C.c_uint8), F, rows, cols, C.byref(cal),
                                   C.byref(sp or sift_params()), C.byref(mp or match_params()),
                                   C.byref(rp or ransac_params()), outs.ctypes.data_as(C.POINTER(StepOut)),
-                                  _p(lm, C.c_double), lm_cap)
+                                  _p(lm, C.c_double), lm_cap, key0)
     return outs, lm[:n].copy()
 
 
@@ -259,3 +265,21 @@ def sift_match_pair(left, right, sp=None, mp=None):
                                      C.byref(sp or sift_params()), C.byref(mp or match_params()),
                                      C.byref(nl), C.byref(nr))
     return S, nl.value, nr.value
+
+
+SPEC_FN = {"expf": 0, "atan2_deg": 1, "sin_deg": 2, "cos_deg": 3, "exp_d": 4, "log_d": 5}
+
+
+def spec_eval(fn: str, x) -> np.ndarray:
+    """Evaluate a vo_spec.h primitive (float ones are computed in float)."""
+    x = np.ascontiguousarray(x, np.float64).reshape(-1)
+    n = x.shape[0] // 2 if fn == "atan2_deg" else x.shape[0]   # atan2 takes (y, x) pairs
+    out = np.zeros(n)
+    lib().oracle_spec_eval(SPEC_FN[fn], _p(x, C.c_double), _p(out, C.c_double), n)
+    return out
+
+
+def philox(ctr, key) -> np.ndarray:
+    out = np.zeros(4, np.uint32)
+    lib().oracle_philox(*[int(v) for v in ctr], int(key[0]), int(key[1]), _p(out, C.c_uint32))
+    return out

@@ -408,12 +408,15 @@ int oracle_sift(const uint8_t* img, int rows, int cols, int ld, const vo_sift_pa
                     float angles[VO_SIFT_MAX_PEAKS + 2];
                     const float* gimg = oc->g[kp.layer];
                     int np = orientations(gimg, R, C, kp.r, kp.c, kp.scl, angles);
+                    /* octave pixel k <-> upsampled pixel 2^o k <-> original 2^o k / 2 - 0.25
+                       (half-pixel-centre x2 upsample); +1 for MATLAB 1-based Location */
                     float oscale = (float)(1 << o) * up_scale;
+                    float loc_off = p->upsample ? 0.75f : 1.0f;
                     for (int a = 0; a < np; ++a) {
                         if (count < capacity) {
                             vo_keypoint* k = &kps[count];
-                            k->x = kp.xo * oscale + 1.0f;
-                            k->y = kp.yo * oscale + 1.0f;
+                            k->x = kp.xo * oscale + loc_off;
+                            k->y = kp.yo * oscale + loc_off;
                             k->size = kp.scl * 2.0f * oscale;
                             k->angle = angles[a];
                             k->response = kp.response;

@@ -547,7 +547,8 @@ static const double I4[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
 
 long oracle_run_sequence(const uint8_t* lefts, const uint8_t* rights, int F, int rows, int cols,
                          const vo_calib* calib, const vo_sift_params* sp, const vo_match_params* mp,
-                         const vo_ransac_params* rp, vo_step_out* outs, double* lm_out, long lm_cap)
+                         const vo_ransac_params* rp, vo_step_out* outs, double* lm_out, long lm_cap,
+                         uint32_t key0)
 {
     int cap = sp->max_keypoints;
     vo_keypoint *kl = malloc(sizeof(vo_keypoint) * cap), *kr = malloc(sizeof(vo_keypoint) * cap);
@@ -593,7 +594,7 @@ long oracle_run_sequence(const uint8_t* lefts, const uint8_t* rights, int F, int
             oracle_triangulate(ol, orr, Kt, calib->P1, calib->P2, wld);
             double T[16];
             int nin = 0;
-            int st = oracle_estworldpose(img, wld, Kt, calib->K, rp, (uint32_t)f, T, NULL, &nin);
+            int st = oracle_estworldpose(img, wld, Kt, calib->K, rp, key0 + (uint32_t)f, T, NULL, &nin);
             o->status = st;
             o->n_inliers = nin;
             if (st == VO_OK) {

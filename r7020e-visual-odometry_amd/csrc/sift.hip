@@ -535,13 +535,15 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
         const int npk = co.npk;
         if (!npk) continue;
         const uint32_t base = koff[(size_t)img * cand_cap + k];
+        // octave pixel k <-> original 2^o k / 2 - 0.25 (half-pixel-centre upsample); +1 = 1-based
         const float oscale = (float)(1 << co.o) * (upsample ? 0.5f : 1.0f);
+        const float loc_off = upsample ? 0.75f : 1.0f;
         for (int p = 0; p < npk; ++p) {
             const uint32_t idx = base + p;
             if (idx >= (uint32_t)kp_cap) break;
             vo_keypoint q;
-            q.x = co.xo * oscale + 1.0f;
-            q.y = co.yo * oscale + 1.0f;
+            q.x = co.xo * oscale + loc_off;
+            q.y = co.yo * oscale + loc_off;
             q.size = co.scl * 2.0f * oscale;
             q.angle = co.ang[p];
             q.response = co.response;

@@ -566,6 +566,13 @@ int vo_reset(vo_ctx* c)
     return VO_OK;
 }
 
+int vo_set_frame_index(vo_ctx* c, long frame_index)
+{
+    if (!c || frame_index < 0) return VO_ERR_ARG;
+    c->frame_index = frame_index;
+    return VO_OK;
+}
+
 // Standalone calls use frame slot 0 and the carry slots: they invalidate the
 // loop state of vo_step (call vo_reset before stepping again).
 static int upload_desc(vo_ctx* c, int slot, const uint8_t* d, int n)

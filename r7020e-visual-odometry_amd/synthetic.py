@@ -85,7 +85,7 @@ def random_scene(seed: int, rows: int, cols: int, f: float = 718.856,
     rng = np.random.default_rng(seed)
     n = int(rng.integers(6, 11)) if n_planes is None else n_planes
     planes = []
-    cu, cv = KITTI00_P0[0, 2], KITTI00_P0[1, 2]
+    cu, cv = KITTI00_P0[0, 2] * f / 718.856, KITTI00_P0[1, 2] * f / 718.856
     for i in range(n):
         z = float(np.exp(rng.uniform(np.log(zmin), np.log(zmax))))
         # frustum extent at depth z
@@ -166,10 +166,20 @@ def yaw(deg: float) -> np.ndarray:
     return np.array([[math.cos(a), 0.0, math.sin(a)], [0.0, 1.0, 0.0], [-math.sin(a), 0.0, math.cos(a)]])
 
 
+def calib(scale: float = 1.0) -> tuple[np.ndarray, np.ndarray]:
+    """KITTI-00 P0/P1 for an image scaled by `scale` (focal and principal point scale,
+    the baseline stays 0.537 m)."""
+    S = np.diag([scale, scale, 1.0])
+    return S @ KITTI00_P0, S @ KITTI00_P1
+
+
 def sequence(n: int, rows: int = 375, cols: int = 1242, seed: int = SEED_BASE, step_m: float = 1.0,
-             yaw_deg: float = 0.3, zmin: float = 20.0, zmax: float = 120.0):
+             yaw_deg: float = 0.3, zmin: float = 20.0, zmax: float = 120.0, scale: float = 1.0):
     """A moving-camera sequence.  Returns (L, R, gt) with gt [n, 4, 4] camera-to-world
-    poses (frame 0 = identity), the quantity VO.m's `pose` estimates."""
+    poses (frame 0 = identity), the quantity VO.m's `pose` estimates.  With
+    scale != 1 the images are rendered with calib(scale) (use rows/cols to match)."""
+    if scale != 1.0:
+        return _sequence_scaled(n, rows, cols, seed, step_m, yaw_deg, zmin, zmax, scale)
     planes = random_scene(seed, rows, cols, zmin=zmin, zmax=zmax, n_planes=10)
     # widen planes so the moving camera keeps seeing texture
     for p in planes[:-1]:
@@ -185,5 +195,32 @@ def sequence(n: int, rows: int = 375, cols: int = 1242, seed: int = SEED_BASE, s
         gt[f, :3, 3] = c
         gt[f, 3, 3] = 1.0
         L[f], R[f] = stereo_pair(seed + 1000 + f, rows, cols, planes=planes, R_wc=Rwc, c_w=c.copy())
+        c = c + Rwc @ np.array([0.0, 0.0, step_m])
+    return L, R, gt
+
+
+def _sequence_scaled(n, rows, cols, seed, step_m, yaw_deg, zmin, zmax, scale):
+    P0, _ = calib(scale)
+    K = P0[:, :3]
+    f = K[0, 0]
+    planes = random_scene(seed, int(round(375 * scale)), int(round(1242 * scale)), f=f, zmin=zmin, zmax=zmax,
+                          n_planes=10, px_per_cell=16.0 * scale)
+    for p in planes[:-1]:
+        cx, w = (p.x0 + p.x1) / 2, (p.x1 - p.x0) * 1.6
+        p.x0, p.x1 = cx - w / 2, cx + w / 2
+    B = baseline_m()
+    L = np.empty((n, rows, cols), np.uint8)
+    R = np.empty((n, rows, cols), np.uint8)
+    gt = np.zeros((n, 4, 4))
+    c = np.zeros(3)
+    for fr in range(n):
+        Rwc = yaw(yaw_deg * fr)
+        gt[fr, :3, :3] = Rwc
+        gt[fr, :3, 3] = c
+        gt[fr, 3, 3] = 1.0
+        left = _render(planes, Rwc, c.copy(), rows, cols, K)
+        right = _render(planes, Rwc, c + Rwc @ np.array([B, 0.0, 0.0]), rows, cols, K)
+        rng = np.random.default_rng((seed + 1000 + fr) ^ 0xABCDEF)
+        L[fr], R[fr] = _to_u8(left, rng, 2.0), _to_u8(right, rng, 2.0)
         c = c + Rwc @ np.array([0.0, 0.0, step_m])
     return L, R, gt

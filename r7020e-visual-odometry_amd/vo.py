@@ -89,7 +89,7 @@ EXPORTS = [
     "vo_set_calib", "vo_last_error", "vo_sift", "vo_match", "vo_track", "vo_triangulate", "vo_estworldpose",
     "vo_landmarks", "vo_step", "vo_step_batch", "vo_step_batch_dev", "vo_get_landmarks", "vo_reset",
     "vo_sift_match_batch_dev", "vo_fetch_keypoints", "vo_fetch_stereo_pairs", "vo_stream", "vo_set_profiling",
-    "vo_kernel_times",
+    "vo_kernel_times", "vo_set_frame_index",
 ]
 
 _lib = None
@@ -138,6 +138,7 @@ def load_library(path: str | os.PathLike | None = None):
     L.vo_step_batch_dev.argtypes = [vp, vp, vp, C.c_int, P(StepOut)]
     L.vo_get_landmarks.argtypes = [vp, P(C.c_double), C.c_int, P(C.c_int)]
     L.vo_reset.argtypes = [vp]
+    L.vo_set_frame_index.argtypes = [vp, C.c_long]
     L.vo_sift_match_batch_dev.argtypes = [vp, vp, vp, C.c_int, P(PairStats)]
     L.vo_fetch_keypoints.argtypes = [vp, C.c_int, P(Keypoint), P(C.c_uint8), C.c_int, P(C.c_int)]
     L.vo_fetch_stereo_pairs.argtypes = [vp, C.c_int, P(C.c_uint32), C.c_int, P(C.c_int)]
@@ -343,6 +344,9 @@ class Context:
 
     def reset(self):
         self._check(self.lib.vo_reset(self.h))
+
+    def set_frame_index(self, idx: int):
+        self._check(self.lib.vo_set_frame_index(self.h, idx))
 
     def set_calib(self, calib: Calib):
         self._check(self.lib.vo_set_calib(self.h, C.byref(calib)))

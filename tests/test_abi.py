@@ -1,0 +1,63 @@
+"""The drop-in boundary: libvo.so exports every entry point include/vo.h
+declares, the Python mirror binds them, the product never touches the oracle,
+and the product fails loudly (no CPU fallback) when the library is absent."""
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+PKG = ROOT / "r7020e-visual-odometry_amd"
+
+
+def header_functions():
+    src = (ROOT / "include" / "vo.h").read_text()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(vo_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = PKG / "lib" / "libvo.so"
+    assert lib.exists(), "build() first"
+    out = subprocess.run(["nm", "-D", "--defined-only", str(lib)], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (vo_\w+)$", out, flags=re.M))
+    missing = [f for f in header_functions() if f not in exported]
+    assert not missing, missing
+
+
+def test_python_mirror_binds_every_symbol(vo):
+    assert sorted(vo.EXPORTS) == header_functions()
+    lib = vo.load_library()
+    for name in vo.EXPORTS:
+        assert hasattr(lib, name)
+
+
+def test_library_is_gfx950_code():
+    lib = PKG / "lib" / "libvo.so"
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)], capture_output=True,
+                         text=True)
+    assert "gfx950" in (out.stdout + out.stderr) or b"gfx950" in lib.read_bytes()
+
+
+def test_product_never_imports_or_links_the_oracle():
+    for p in list(PKG.rglob("*.py")) + list(PKG.rglob("*.hip")) + list(PKG.rglob("*.h")) + [PKG / "csrc" / "Makefile"]:
+        text = p.read_text()
+        for needle in ("liboracle", "import oracle", "from oracle", '#include "oracle', "oracle.h"):
+            assert needle not in text, (p, needle)   # comments citing oracle/*.c for op order are fine
+    out = subprocess.run(["ldd", str(PKG / "lib" / "libvo.so")], capture_output=True, text=True).stdout
+    assert "oracle" not in out
+
+
+def test_no_gpu_means_loud_failure(vo):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(vo.VOError):
+        vo.Context(375, 1242, 1)
+
+
+def test_missing_library_raises(vo, tmp_path, monkeypatch):
+    monkeypatch.setattr(vo, "_lib", None)
+    with pytest.raises(vo.VOError):
+        vo.load_library(tmp_path / "nope.so")

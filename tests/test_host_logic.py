@@ -1,0 +1,35 @@
+"""Host-side logic: frame sharding, the pose chain, the roofline byte model."""
+import numpy as np
+import pytest
+
+
+def test_shard_range_partitions(vo_pkg=None):
+    from r7020e_visual_odometry_amd import sharding
+    for n in (1, 7, 64, 4541):
+        for w in (1, 2, 3, 8):
+            spans = [sharding.shard_range(n, w, r) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            for (a, b), (c, d) in zip(spans, spans[1:]):
+                assert b == c
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+    assert sharding.halo_start(0) == 0 and sharding.halo_start(5) == 4
+
+
+def test_chain_matches_oracle_sequence(oracle, syn):
+    from r7020e_visual_odometry_amd import sharding
+    z = np.load(__import__("pathlib").Path(__file__).resolve().parent / "golden" / "sequence.npz")
+    rel = z["out_rel_pose"]
+    assert np.array_equal(sharding.chain(rel), z["out_pose"])
+
+
+def test_roofline_model_matches_survey():
+    from r7020e_visual_odometry_amd import roofline
+    dims = roofline.octave_dims(375, 1242)
+    assert len(dims) == 9 and dims[0] == (750, 2484)
+    P = sum(r * c for r, c in dims)
+    assert abs(P - 2.483e6) / 2.483e6 < 0.01                       # P = 2.483 Mpx
+    per_frame = 2 * roofline.pyramid_bytes_per_image(375, 1242)
+    assert abs(per_frame - 438e6) / 438e6 < 0.01                    # 438 MB / stereo frame
+    kb = roofline.kernel_bytes(375, 1242, 2)
+    assert kb["k_blur_v<true>"][1] == 9 * 5 and kb["k_blur_h"][1] == 9 * 5
