@@ -112,7 +112,7 @@ def main():
     else:
         roof.update({"achieved": None, "frac": None, "bytes_per_launch": None})
     # whole-pyramid figure (SURVEY §8(d) per-frame model over the pyramid kernels' time)
-    pyr_names = [n for n in kt if n.startswith(("k_base_h", "k_blur_h", "k_blur_v", "k_down"))]
+    pyr_names = [n for n in kt if n.startswith(("k_blur", "k_down"))]
     pyr_ms = sum(kt[n][0] for n in pyr_names) / args.profile_steps
     pyr_bytes = 2 * B * roofline.pyramid_bytes_per_image(ROWS, COLS)
     roof["pyramid_model_gbs"] = pyr_bytes / (pyr_ms * 1e-3) / 1e9 if pyr_ms > 0 else None

@@ -1,15 +1,14 @@
 // sift.hip — detectSIFTFeatures + extractFeatures (VO.m:79-84) on gfx950.
 //
-// Pipeline per batch of n_img images (DESIGN.md §5.1):
-//   k_base_h / k_blur_h   horizontal Gaussian pass, row tile staged in LDS
-//                         (octave 0 computes the x2 upsample on the fly)
-//   k_blur_v              vertical pass from an LDS column tile; writes G_i and
-//                         the DoG D_{i-1} = G_i - G_{i-1} in the same pass
+// Pipeline per batch of n_img images (DESIGN.md §5):
+//   k_blur_fused          one launch per scale level: row + column Gaussian
+//                         passes through one LDS tile, writes G_i and the DoG
+//                         D_{i-1} = G_i - G_{i-1} (octave 0: x2 upsample fused)
 //   k_down                next octave base = G[o-1][L](2y, 2x)
-//   k_ext_mask            26-neighbour extremum test, one wave per 64 columns,
-//                         ballot -> 64-bit mask per word
-//   k_scan_words/k_emit   deterministic compaction in (octave, layer, row, col)
-//                         scan order (prefix sum, no atomic append)
+//   k_ext_tile            26-neighbour extremum test on LDS tiles of all DoG
+//                         levels, ballot -> 64-bit mask per 64 columns
+//   k_seg_count/scan/emit deterministic compaction in (octave, layer, row,
+//                         col) scan order (prefix sums, no atomic append)
 //   k_refine_orient       one wave per candidate: Newton refinement (wave-
 //                         uniform), orientation histogram (lanes stride the
 //                         window, 2^-20 fixed-point LDS atomics), peaks by ballot
@@ -20,6 +19,7 @@
 #include "vo_internal.h"
 #include <cstring>
 #include <cmath>
+#include <algorithm>
 
 namespace vo {
 
@@ -64,6 +64,16 @@ void build_pyramid_geometry(Pyramid& py, int rows, int cols, int n_img, const vo
     }
     py.wbase[b] = w;
     py.n_words = w;
+    int t = 0;
+    for (int o = 0; o < py.n_oct; ++o) {
+        int ir = py.oct[o].rows - 2 * VO_SIFT_BORDER;
+        if (ir < 0) ir = 0;
+        py.tbase[o] = t;
+        t += (ir + VO_EXT_TILE_ROWS - 1) / VO_EXT_TILE_ROWS * py.wrow[o];
+    }
+    py.tbase[py.n_oct] = t;
+    py.n_tiles = t;
+    py.n_seg = (w + VO_SEG_WORDS - 1) / VO_SEG_WORDS;
 }
 
 hipError_t sift_alloc(SiftBuffers& b, const Pyramid& py, int kp_cap, int cand_cap)
@@ -75,7 +85,7 @@ hipError_t sift_alloc(SiftBuffers& b, const Pyramid& py, int kp_cap, int cand_ca
     VO_ALLOC(b.arena, sizeof(float) * py.total);
     VO_ALLOC(b.tmp, sizeof(float) * py.tmp_plane * n);
     VO_ALLOC(b.mask, sizeof(unsigned long long) * (size_t)py.n_words * n + 8);
-    VO_ALLOC(b.woff, sizeof(uint32_t) * (size_t)py.n_words * n + 8);
+    VO_ALLOC(b.woff, sizeof(uint32_t) * (size_t)py.n_seg * n + 8);
     VO_ALLOC(b.cand, sizeof(uint32_t) * (size_t)cand_cap * n);
     VO_ALLOC(b.n_cand, sizeof(int) * n);
     VO_ALLOC(b.cout, sizeof(CandOut) * (size_t)cand_cap * n);
@@ -99,8 +109,6 @@ void sift_free(SiftBuffers& b)
 // ---------------------------------------------------------------------------
 // Gaussian pyramid
 // ---------------------------------------------------------------------------
-#define HB 256   // outputs per block of the horizontal pass
-
 __device__ __forceinline__ float up_sample(const uint8_t* __restrict__ img, int ld, int rows, int cols, int y, int x)
 {
     int ya = y >> 1, yb = (y & 1) ? (ya + 1 < rows ? ya + 1 : rows - 1) : (ya > 0 ? ya - 1 : 0);
@@ -110,72 +118,220 @@ __device__ __forceinline__ float up_sample(const uint8_t* __restrict__ img, int 
     return 0.75f * ha + 0.25f * hb;
 }
 
-// octave-0 base: (upsample) + horizontal pass.  grid (ceil(C/HB), R, n_img)
-template <bool UP>
-__global__ __launch_bounds__(HB) void k_base_h(ImageSrc src, int rows, int cols, int R, int C, float* __restrict__ tmp,
-                                               size_t tmp_plane, int tpitch, Kern K)
+// ---------------------------------------------------------------------------
+// Fused separable blur of one scale level + DoG (one launch per level).
+// A 64x64 output tile and its radius-r halo are staged once in LDS; the row
+// pass writes a (64+2r) x 64 LDS image, the column pass writes G_i and
+// D_{i-1} = G_i - G_{i-1} (G_{i-1} is the tile centre already in LDS).
+// Register blocking: each thread produces 8 consecutive outputs along the
+// filter direction from 8+2r values loaded once (LDS reads / output ~10
+// instead of ~54).  RAD > 0 instantiates the radius (full unroll, static
+// register indices); RAD == 0 is the generic runtime-radius path.
+// MODE 0: float source plane (+DoG); 1: octave-0 base from the u8 image with
+// the x2 upsample computed on the fly; 2: octave-0 base from u8, no upsample.
+// Accumulation order per output = oracle_blur: acc = k0*s0;
+// acc = fmaf(kj, s[-j] + s[+j], acc), j = 1..r (row pass, then column pass).
+// ---------------------------------------------------------------------------
+#define FT_W 64
+#define FT_H 64
+#define FT_V 8            // outputs per thread along the filter direction
+#define FT_HW (FT_W + 4)  // row-pass LDS row stride: +4 floats breaks the 8-way b128 store conflict
+
+__host__ __device__ constexpr int ft_iw(int r) { return (FT_W + 2 * r + 3) & ~3; }   // padded to 16 B
+__host__ __device__ constexpr int ft_lds_floats(int r) { return (FT_H + 2 * r) * ft_iw(r) + (FT_H + 2 * r) * FT_HW; }
+
+template <int RAD, int MODE>
+__global__ __launch_bounds__(256) void k_blur_fused(const float* __restrict__ src, size_t plane, int pitch, int R, int C,
+                                                    float* __restrict__ g_out, float* __restrict__ d_out, Kern K,
+                                                    ImageSrc isrc, int in_rows, int in_cols)
 {
-    __shared__ float buf[HB + 2 * VO_SIFT_MAX_RADIUS];
-    const int img = blockIdx.z, y = blockIdx.y, x0 = blockIdx.x * HB, r = K.r;
-    const uint8_t* base = ((img & 1) ? src.right : src.left) + (size_t)(img >> 1) * src.frame_stride;
-    for (int t = threadIdx.x; t < HB + 2 * r; t += HB) {
-        int x = vo_reflect101(x0 - r + t, C);
-        buf[t] = UP ? up_sample(base, src.ld, rows, cols, y, x) : (float)base[y * src.ld + x];
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int r = RAD > 0 ? RAD : K.r;
+    const int IW = ft_iw(r), IH = FT_H + 2 * r;
+    float* in = sm;
+    float* hb = sm + IH * IW;
+    const int img = blockIdx.z, x0 = blockIdx.x * FT_W, y0 = blockIdx.y * FT_H, tid = threadIdx.x;
+    const uint8_t* base8 = nullptr;
+    if (MODE != 0) base8 = ((img & 1) ? isrc.right : isrc.left) + (size_t)(img >> 1) * isrc.frame_stride;
+    const float* srcp = src + img * plane;
+    // ---- stage the input tile (reflect-101 only for tiles touching a border) ----
+    const int LW = FT_W + 2 * r;
+    const int ylo = y0 - r, xlo = x0 - r;
+    const bool interior = ylo >= 0 && y0 + FT_H + r <= R && xlo >= 0 && x0 + FT_W + r <= C;
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int rr = wv; rr < IH; rr += 4) {
+        const int y = interior ? ylo + rr : vo_reflect101(ylo + rr, R);
+        for (int cc = lane; cc < LW; cc += 64) {
+            const int x = interior ? xlo + cc : vo_reflect101(xlo + cc, C);
+            float v;
+            if (MODE == 0) v = srcp[(size_t)y * pitch + x];
+            else if (MODE == 1) v = up_sample(base8, isrc.ld, in_rows, in_cols, y, x);
+            else v = (float)base8[y * isrc.ld + x];
+            in[rr * IW + cc] = v;
+        }
     }
     __syncthreads();
-    int x = x0 + threadIdx.x;
-    if (x >= C) return;
-    const float* s = buf + threadIdx.x + r;
-    float acc = K.k[0] * s[0];
-    for (int j = 1; j <= r; ++j) acc = fmaf(K.k[j], s[-j] + s[j], acc);
-    tmp[img * tmp_plane + (size_t)y * tpitch + x] = acc;
-}
-
-// horizontal pass on a float plane.  grid (ceil(C/HB), R, n_img)
-__global__ __launch_bounds__(HB) void k_blur_h(const float* __restrict__ src, size_t plane, int pitch, int R, int C,
-                                               float* __restrict__ tmp, size_t tmp_plane, Kern K)
-{
-    __shared__ float buf[HB + 2 * VO_SIFT_MAX_RADIUS];
-    const int img = blockIdx.z, y = blockIdx.y, x0 = blockIdx.x * HB, r = K.r;
-    const float* row = src + img * plane + (size_t)y * pitch;
-    for (int t = threadIdx.x; t < HB + 2 * r; t += HB) buf[t] = row[vo_reflect101(x0 - r + t, C)];
-    __syncthreads();
-    int x = x0 + threadIdx.x;
-    if (x >= C) return;
-    const float* s = buf + threadIdx.x + r;
-    float acc = K.k[0] * s[0];
-    for (int j = 1; j <= r; ++j) acc = fmaf(K.k[j], s[-j] + s[j], acc);
-    tmp[img * tmp_plane + (size_t)y * pitch + x] = acc;
-}
-
-#define VT_W 64
-#define VT_H 32
-// vertical pass + DoG.  block (64,4), grid (ceil(C/64), ceil(R/32), n_img)
-template <bool DOG>
-__global__ __launch_bounds__(256) void k_blur_v(const float* __restrict__ tmp, size_t tmp_plane, int pitch, int R, int C,
-                                                float* __restrict__ g_out, const float* __restrict__ g_prev,
-                                                float* __restrict__ d_out, size_t plane, Kern K)
-{
-    __shared__ float tile[(VT_H + 2 * VO_SIFT_MAX_RADIUS) * VT_W];
-    const int img = blockIdx.z, x0 = blockIdx.x * VT_W, y0 = blockIdx.y * VT_H, r = K.r;
-    const int tx = threadIdx.x, ty = threadIdx.y;
-    const int x = x0 + tx;
-    const float* src = tmp + img * tmp_plane;
-    for (int rr = ty; rr < VT_H + 2 * r; rr += 4) {
-        int y = vo_reflect101(y0 - r + rr, R);
-        tile[rr * VT_W + tx] = x < C ? src[(size_t)y * pitch + x] : 0.0f;
+    // ---- row pass: IH rows x 64 columns, 8 consecutive columns per item ----
+    for (int t = tid; t < IH * (FT_W / FT_V); t += 256) {
+        const int rr = t >> 3, c0 = (t & 7) * FT_V;
+        const float* s = in + rr * IW + c0;            // s[k] = input column c0 - r + k
+        float out[FT_V];
+        if constexpr (RAD > 0) {
+            float v[FT_V + 2 * RAD];
+#pragma unroll
+            for (int k = 0; k < FT_V + 2 * RAD; ++k) v[k] = s[k];
+#pragma unroll
+            for (int i = 0; i < FT_V; ++i) {
+                float acc = K.k[0] * v[i + RAD];
+#pragma unroll
+                for (int j = 1; j <= RAD; ++j) acc = fmaf(K.k[j], v[i + RAD - j] + v[i + RAD + j], acc);
+                out[i] = acc;
+            }
+        } else {
+            for (int i = 0; i < FT_V; ++i) {
+                const float* q = s + i + r;
+                float acc = K.k[0] * q[0];
+                for (int j = 1; j <= r; ++j) acc = fmaf(K.k[j], q[-j] + q[j], acc);
+                out[i] = acc;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < FT_V; ++i) hb[rr * FT_HW + c0 + i] = out[i];
     }
     __syncthreads();
-    if (x >= C) return;
-    for (int q = 0; q < VT_H / 4; ++q) {
-        int yl = ty + 4 * q, y = y0 + yl;
-        if (y >= R) break;
-        const float* s = tile + (yl + r) * VT_W + tx;
-        float acc = K.k[0] * s[0];
-        for (int j = 1; j <= r; ++j) acc = fmaf(K.k[j], s[-j * VT_W] + s[j * VT_W], acc);
-        size_t o = img * plane + (size_t)y * pitch + x;
-        g_out[o] = acc;
-        if (DOG) d_out[o] = acc - g_prev[o];
+    // ---- column pass: 64 columns x (64/8) row groups ----
+    for (int t = tid; t < FT_W * (FT_H / FT_V); t += 256) {
+        const int c = t & 63, y0l = (t >> 6) * FT_V;
+        const int x = x0 + c;
+        const float* s = hb + y0l * FT_HW + c;         // s[k*FT_HW] = row-pass row y0l - r + k (tile coords + r)
+        float out[FT_V];
+        if constexpr (RAD > 0) {
+            float v[FT_V + 2 * RAD];
+#pragma unroll
+            for (int k = 0; k < FT_V + 2 * RAD; ++k) v[k] = s[k * FT_HW];
+#pragma unroll
+            for (int i = 0; i < FT_V; ++i) {
+                float acc = K.k[0] * v[i + RAD];
+#pragma unroll
+                for (int j = 1; j <= RAD; ++j) acc = fmaf(K.k[j], v[i + RAD - j] + v[i + RAD + j], acc);
+                out[i] = acc;
+            }
+        } else {
+            for (int i = 0; i < FT_V; ++i) {
+                const float* q = s + (i + r) * FT_HW;
+                float acc = K.k[0] * q[0];
+                for (int j = 1; j <= r; ++j) acc = fmaf(K.k[j], q[-j * FT_HW] + q[j * FT_HW], acc);
+                out[i] = acc;
+            }
+        }
+        if (x < C) {
+#pragma unroll
+            for (int i = 0; i < FT_V; ++i) {
+                const int y = y0 + y0l + i;
+                if (y < R) {
+                    const size_t o = img * plane + (size_t)y * pitch + x;
+                    g_out[o] = out[i];
+                    if (MODE == 0) d_out[o] = out[i] - in[(y0l + i + r) * IW + c + r];
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Persistent, software-pipelined level blur (MODE 0, compiled radius).  Same
+// per-output arithmetic as k_blur_fused; each block walks tiles
+// T, T+grid, ...: the global loads of tile T+grid are issued into registers
+// right after tile T is in LDS, so they are in flight during T's row and
+// column passes (async-STAGE split), instead of every tile exposing a full
+// HBM round trip behind a barrier.
+// ---------------------------------------------------------------------------
+template <int RAD>
+__global__ __launch_bounds__(256) void k_blur_pipe(const float* __restrict__ src, size_t plane, int pitch, int R, int C,
+                                                   float* __restrict__ g_out, float* __restrict__ d_out, Kern K,
+                                                   int tiles_x, int tiles_y, int n_tiles)
+{
+    constexpr int IW = ft_iw(RAD), IH = FT_H + 2 * RAD, LW = FT_W + 2 * RAD;
+    constexpr int NE = IH * LW, NQ = (NE + 255) / 256;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* in = sm;
+    float* hb = sm + IH * IW;
+    const int tid = threadIdx.x;
+    const int tpi = tiles_x * tiles_y;
+    float pre[NQ];
+    auto fetch = [&](int T) {
+        const int img = T / tpi, rem = T - img * tpi;
+        const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
+        const int ylo = ty * FT_H - RAD, xlo = tx * FT_W - RAD;
+        const bool interior = ylo >= 0 && ylo + IH <= R && xlo >= 0 && xlo + LW <= C;
+        const float* sp = src + img * plane;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int e = tid + 256 * q;
+            if (e < NE) {
+                const int rr = e / LW, cc = e - rr * LW;
+                const int y = interior ? ylo + rr : vo_reflect101(ylo + rr, R);
+                const int x = interior ? xlo + cc : vo_reflect101(xlo + cc, C);
+                pre[q] = sp[(size_t)y * pitch + x];
+            }
+        }
+    };
+    int T = blockIdx.x;
+    if (T < n_tiles) fetch(T);
+    for (; T < n_tiles; T += gridDim.x) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int e = tid + 256 * q;
+            if (e < NE) {
+                const int rr = e / LW, cc = e - rr * LW;
+                in[rr * IW + cc] = pre[q];
+            }
+        }
+        __syncthreads();
+        if (T + (int)gridDim.x < n_tiles) fetch(T + gridDim.x);
+        // ---- row pass ----
+        for (int t = tid; t < IH * (FT_W / FT_V); t += 256) {
+            const int rr = t >> 3, c0 = (t & 7) * FT_V;
+            const float* s = in + rr * IW + c0;
+            float v[FT_V + 2 * RAD];
+#pragma unroll
+            for (int k = 0; k < FT_V + 2 * RAD; ++k) v[k] = s[k];
+#pragma unroll
+            for (int i = 0; i < FT_V; ++i) {
+                float acc = K.k[0] * v[i + RAD];
+#pragma unroll
+                for (int j = 1; j <= RAD; ++j) acc = fmaf(K.k[j], v[i + RAD - j] + v[i + RAD + j], acc);
+                hb[rr * FT_HW + c0 + i] = acc;
+            }
+        }
+        __syncthreads();
+        // ---- column pass + G/DoG stores ----
+        const int img = T / tpi, rem = T - img * tpi;
+        const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
+        const int x0 = tx * FT_W, y0 = ty * FT_H;
+        for (int t = tid; t < FT_W * (FT_H / FT_V); t += 256) {
+            const int c = t & 63, y0l = (t >> 6) * FT_V;
+            const int x = x0 + c;
+            const float* s = hb + y0l * FT_HW + c;
+            float v[FT_V + 2 * RAD];
+#pragma unroll
+            for (int k = 0; k < FT_V + 2 * RAD; ++k) v[k] = s[k * FT_HW];
+            if (x < C) {
+#pragma unroll
+                for (int i = 0; i < FT_V; ++i) {
+                    float acc = K.k[0] * v[i + RAD];
+#pragma unroll
+                    for (int j = 1; j <= RAD; ++j) acc = fmaf(K.k[j], v[i + RAD - j] + v[i + RAD + j], acc);
+                    const int y = y0 + y0l + i;
+                    if (y < R) {
+                        const size_t o = img * plane + (size_t)y * pitch + x;
+                        g_out[o] = acc;
+                        d_out[o] = acc - in[(y0l + i + RAD) * IW + c + RAD];
+                    }
+                }
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -209,49 +365,114 @@ __device__ __forceinline__ void decode_word(const Pyramid* __restrict__ py, int 
     k = rel - (rel / wr) * wr;
 }
 
-// one wave per word.  block 256 (4 words), grid-stride
-__global__ __launch_bounds__(256) void k_ext_mask(const Pyramid* __restrict__ py, const float* __restrict__ arena,
-                                                  unsigned long long* __restrict__ mask, int n_img, float thr)
+// ---------------------------------------------------------------------------
+// 26-neighbour extremum test.  One block per tile of 64 interior columns x 16
+// interior rows of one octave; the tile (+1 halo) of all L+2 DoG levels is
+// staged in LDS once and serves all L layers (DoG read once, not 3x).  Wave w
+// owns tile rows 4w..4w+3; each lane keeps its 6x3 window of every level in
+// registers and tests 4 rows x L layers; one ballot per (row, layer) is the
+// 64-bit mask word of that row in (octave, layer, row, word) order.
+// ---------------------------------------------------------------------------
+#define ET_W 64
+#define ET_LW 68            // LDS row length (66 used)
+#define ET_LR (VO_EXT_TILE_ROWS + 2)
+
+template <int L>
+__global__ __launch_bounds__(256) void k_ext_tile(const Pyramid* __restrict__ py, const float* __restrict__ arena,
+                                                  unsigned long long* __restrict__ mask, float thr, int n_img)
 {
-    const int lane = threadIdx.x & 63;
-    const int nw = py->n_words;
-    const long total = (long)nw * n_img;
-    for (long t = (long)blockIdx.x * 4 + (threadIdx.x >> 6); t < total; t += (long)gridDim.x * 4) {
-        const int img = (int)(t / nw), w = (int)(t - (long)img * nw);
-        int o, layer, r, k;
-        decode_word(py, w, o, layer, r, k);
-        const OctGeom& g = py->oct[o];
-        const int c = VO_SIFT_BORDER + 64 * k + lane;
-        bool ext = false;
-        if (c < g.cols - VO_SIFT_BORDER) {
-            const float* cur = arena + g.d_off[layer] + img * g.plane + (size_t)r * g.pitch + c;
-            const float* prv = arena + g.d_off[layer - 1] + img * g.plane + (size_t)r * g.pitch + c;
-            const float* nxt = arena + g.d_off[layer + 1] + img * g.plane + (size_t)r * g.pitch + c;
-            const float val = cur[0];
-            if (fabsf(val) > thr) {
-                ext = true;
-                const int P = g.pitch;
-                if (val > 0) {
+    __shared__ float lds[(L + 2) * ET_LR * ET_LW];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nt = py->n_tiles, total = nt * n_img;
+    // persistent: block walks tiles T, T+grid, ...
+    auto locate = [&](int T, int& img, int& o, int& k, int& r0, int& c0) {
+        img = T / nt;
+        const int t = T - img * nt;
+        o = 0;
+        while (o + 1 < py->n_oct && py->tbase[o + 1] <= t) ++o;
+        const int wr = py->wrow[o], rel = t - py->tbase[o];
+        const int rb = rel / wr;
+        k = rel - rb * wr;
+        r0 = VO_SIFT_BORDER + rb * VO_EXT_TILE_ROWS;
+        c0 = VO_SIFT_BORDER + k * ET_W;
+    };
+    for (int T = blockIdx.x; T < total; T += gridDim.x) {
+        {
+            int img, o, k, r0, c0;
+            locate(T, img, o, k, r0, c0);
+            const OctGeom& g = py->oct[o];
+            // all loads issued back to back (level loop uniform -> scalar plane bases), then LDS writes
+            constexpr int PE = ET_LR * (ET_W + 2), PQ = (PE + 255) / 256;
+            int off[PQ];
 #pragma unroll
-                    for (int dy = -1; dy <= 1; ++dy)
+            for (int q = 0; q < PQ; ++q) {
+                const int e = tid + 256 * q;
+                const int rr = e / (ET_W + 2), cc = e - rr * (ET_W + 2);
+                off[q] = min(r0 - 1 + rr, g.rows - 1) * g.pitch + min(c0 - 1 + cc, g.cols - 1);
+            }
+            float tv[L + 2][PQ];
 #pragma unroll
-                        for (int dx = -1; dx <= 1; ++dx) {
-                            const int q = dy * P + dx;
-                            ext = ext && (val >= prv[q]) && (val >= nxt[q]) && (val >= cur[q]);
-                        }
-                } else {
+            for (int lv = 0; lv < L + 2; ++lv) {
+                const float* pl = arena + g.d_off[lv] + img * g.plane;
 #pragma unroll
-                    for (int dy = -1; dy <= 1; ++dy)
+                for (int q = 0; q < PQ; ++q)
+                    if (tid + 256 * q < PE) tv[lv][q] = pl[off[q]];
+            }
 #pragma unroll
-                        for (int dx = -1; dx <= 1; ++dx) {
-                            const int q = dy * P + dx;
-                            ext = ext && (val <= prv[q]) && (val <= nxt[q]) && (val <= cur[q]);
-                        }
+            for (int lv = 0; lv < L + 2; ++lv)
+#pragma unroll
+                for (int q = 0; q < PQ; ++q) {
+                    const int e = tid + 256 * q;
+                    if (e < PE) {
+                        const int rr = e / (ET_W + 2), cc = e - rr * (ET_W + 2);
+                        lds[(lv * ET_LR + rr) * ET_LW + cc] = tv[lv][q];
+                    }
                 }
+        }
+        __syncthreads();
+        int img, o, k, r0, c0;
+        locate(T, img, o, k, r0, c0);
+        const OctGeom& g = py->oct[o];
+        const int wr = py->wrow[o];
+        const int c = c0 + lane;
+        const bool cval = c < g.cols - VO_SIFT_BORDER;
+        // 3x3 max/min of every DoG level at this lane's column for the wave's 4 rows.
+        // val >= all 26 neighbours  <=>  val >= max of the 3x3x3 block (val included),
+        // and the per-level 3x3 extrema are shared by the adjacent layers.
+        float mx3[L + 2][4], mn3[L + 2][4], ctr[L + 2][4];
+#pragma unroll
+        for (int lv = 0; lv < L + 2; ++lv) {
+            float hmx[6], hmn[6];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                const float* row = lds + (lv * ET_LR + 4 * w + a) * ET_LW + lane;
+                const float x0 = row[0], x1 = row[1], x2 = row[2];
+                hmx[a] = fmaxf(fmaxf(x0, x1), x2);
+                hmn[a] = fminf(fminf(x0, x1), x2);
+                if (a >= 1 && a <= 4) ctr[lv][a - 1] = x1;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                mx3[lv][q] = fmaxf(fmaxf(hmx[q], hmx[q + 1]), hmx[q + 2]);
+                mn3[lv][q] = fminf(fminf(hmn[q], hmn[q + 1]), hmn[q + 2]);
             }
         }
-        unsigned long long b = __ballot(ext);
-        if (lane == 0) mask[t] = b;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = r0 + 4 * w + q;
+            const bool rval = r < g.rows - VO_SIFT_BORDER;
+#pragma unroll
+            for (int layer = 1; layer <= L; ++layer) {
+                const float val = ctr[layer][q];
+                const float bmx = fmaxf(fmaxf(mx3[layer - 1][q], mx3[layer][q]), mx3[layer + 1][q]);
+                const float bmn = fminf(fminf(mn3[layer - 1][q], mn3[layer][q]), mn3[layer + 1][q]);
+                const bool ext = fabsf(val) > thr && ((val > 0 && val >= bmx) || (!(val > 0) && val <= bmn));
+                const unsigned long long bal = __ballot(ext && cval);
+                if (lane == 0 && rval)
+                    mask[(size_t)img * py->n_words + py->wbase[o * L + layer - 1] + (size_t)(r - VO_SIFT_BORDER) * wr + k] = bal;
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -283,39 +504,82 @@ __device__ __forceinline__ uint32_t block_exscan_1024(uint32_t v, uint32_t* sh, 
     return before + x - v;
 }
 
-// per image: exclusive scan of popcount(mask) -> woff, n_cand.  grid n_img, block 1024
-__global__ __launch_bounds__(1024) void k_scan_words(const unsigned long long* __restrict__ mask, uint32_t* __restrict__ woff,
-                                                     int* __restrict__ n_cand, int nw)
+// Compaction in (octave, layer, row, column) order, three coalesced passes:
+// per-segment popcounts (1024 words), per-image exclusive scan of segments,
+// then each segment block scans its words and emits candidates.
+__global__ __launch_bounds__(256) void k_seg_count(const unsigned long long* __restrict__ mask, uint32_t* __restrict__ segc,
+                                                   int nw, int nseg)
+{
+    __shared__ uint32_t red[4];
+    const int img = blockIdx.y, seg = blockIdx.x, tid = threadIdx.x;
+    const unsigned long long* m = mask + (size_t)img * nw;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int wd = seg * VO_SEG_WORDS + q * 256 + tid;
+        if (wd < nw) cnt += (uint32_t)__popcll(m[wd]);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+    if ((tid & 63) == 0) red[tid >> 6] = cnt;
+    __syncthreads();
+    if (tid == 0) segc[(size_t)img * nseg + seg] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(1024) void k_seg_scan(uint32_t* __restrict__ segc, int* __restrict__ n_cand, int nseg)
 {
     __shared__ uint32_t sh[32];
     const int img = blockIdx.x, tid = threadIdx.x;
-    const unsigned long long* m = mask + (size_t)img * nw;
-    uint32_t* wo = woff + (size_t)img * nw;
-    const int chunk = (nw + 1023) / 1024;
-    const int a = tid * chunk, e = min(a + chunk, nw);
-    uint32_t s = 0;
-    for (int w = a; w < e; ++w) s += (uint32_t)__popcll(m[w]);
+    uint32_t v = tid < nseg ? segc[(size_t)img * nseg + tid] : 0u;
     uint32_t total;
-    uint32_t base = block_exscan_1024(s, sh, &total);
-    for (int w = a; w < e; ++w) { wo[w] = base; base += (uint32_t)__popcll(m[w]); }
+    const uint32_t ex = block_exscan_1024(v, sh, &total);
+    if (tid < nseg) segc[(size_t)img * nseg + tid] = ex;
     if (tid == 0) n_cand[img] = (int)total;
 }
 
-__global__ void k_emit(const Pyramid* __restrict__ py, const unsigned long long* __restrict__ mask,
-                       const uint32_t* __restrict__ woff, uint32_t* __restrict__ cand, int cand_cap, int n_img)
+__device__ __forceinline__ uint32_t block_exscan_256(uint32_t v, uint32_t* sh)
 {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int q = 0; q < wid; ++q) before += sh[q];
+    return before + x - v;
+}
+
+__global__ __launch_bounds__(256) void k_seg_emit(const Pyramid* __restrict__ py, const unsigned long long* __restrict__ mask,
+                                                  const uint32_t* __restrict__ segoff, uint32_t* __restrict__ cand,
+                                                  int cand_cap)
+{
+    __shared__ uint32_t sh[4];
+    const int img = blockIdx.y, seg = blockIdx.x, tid = threadIdx.x;
     const int nw = py->n_words;
-    const long total = (long)nw * n_img;
-    for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-        unsigned long long m = mask[t];
-        if (!m) continue;
-        const int img = (int)(t / nw), w = (int)(t - (long)img * nw);
+    const unsigned long long* m = mask + (size_t)img * nw;
+    const int w0 = seg * VO_SEG_WORDS + tid * 4;     // 4 consecutive words per thread
+    unsigned long long mw[4];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        mw[q] = (w0 + q < nw) ? m[w0 + q] : 0ull;
+        cnt += (uint32_t)__popcll(mw[q]);
+    }
+    uint32_t idx = segoff[(size_t)img * py->n_seg + seg] + block_exscan_256(cnt, sh);
+    if (!cnt) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        unsigned long long mm = mw[q];
+        if (!mm) continue;
         int o, layer, r, k;
-        decode_word(py, w, o, layer, r, k);
-        uint32_t idx = woff[t];
-        while (m) {
-            int bit = __ffsll((long long)m) - 1;
-            m &= m - 1;
+        decode_word(py, w0 + q, o, layer, r, k);
+        while (mm) {
+            const int bit = __ffsll((long long)mm) - 1;
+            mm &= mm - 1;
             if (idx < (uint32_t)cand_cap) cand[(size_t)img * cand_cap + idx] = pack_cand(o, layer, r, VO_SIFT_BORDER + 64 * k + bit);
             idx++;
         }
@@ -691,6 +955,54 @@ static Kern make_kern(const Pyramid& py, int level)
     return k;
 }
 
+template <int RAD, int MODE>
+static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t plane, int pitch, int R, int C, float* g,
+                          float* d, const Kern& K, const ImageSrc& isrc, int in_rows, int in_cols)
+{
+    const size_t lds = sizeof(float) * ft_lds_floats(K.r);
+    if (MODE == 0 && RAD > 0) {
+        // persistent grid: as many blocks as can be co-resident, walking all tiles
+        static int per_cu = 0;
+        if (!per_cu) {
+            if (lds > 64 * 1024)
+                hipFuncSetAttribute((const void*)k_blur_pipe<RAD>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_blur_pipe<RAD>, 256, lds);
+            if (per_cu < 1) per_cu = 1;
+        }
+        int dev = 0, cus = 256;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const int n_tiles = grid.x * grid.y * grid.z;
+        const int blocks = std::min(n_tiles, per_cu * cus);
+        VO_LAUNCH_NAMED("k_blur_fused", k_blur_pipe<RAD>, dim3(blocks), dim3(256), lds, s, src, plane, pitch, R, C, g, d, K,
+                        (int)grid.x, (int)grid.y, n_tiles);
+        return;
+    }
+    if (lds > 64 * 1024) {
+        static bool once = false;
+        if (!once) {
+            hipFuncSetAttribute((const void*)k_blur_fused<RAD, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            once = true;
+        }
+    }
+    VO_LAUNCH_NAMED(MODE == 0 ? "k_blur_fused" : "k_blur_base", (k_blur_fused<RAD, MODE>), grid, dim3(256), lds, s, src,
+                    plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols);
+}
+
+template <int MODE>
+static void launch_blur(dim3 grid, hipStream_t s, const float* src, size_t plane, int pitch, int R, int C, float* g,
+                        float* d, const Kern& K, const ImageSrc& isrc, int in_rows, int in_cols)
+{
+    switch (K.r) {
+    case 5: launch_blur_r<5, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols); break;
+    case 6: launch_blur_r<6, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols); break;
+    case 8: launch_blur_r<8, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols); break;
+    case 10: launch_blur_r<10, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols); break;
+    case 13: launch_blur_r<13, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols); break;
+    default: launch_blur_r<0, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols); break;
+    }
+}
+
 void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img, const vo_sift_params& p,
                   hipStream_t s, const Pyramid* d_py)
 {
@@ -699,15 +1011,12 @@ void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_
     for (int o = 0; o < py.n_oct; ++o) {
         const OctGeom& g = py.oct[o];
         const int R = g.rows, C = g.cols;
-        dim3 gh((C + HB - 1) / HB, R, n_img), bh(HB);
-        dim3 gv((C + VT_W - 1) / VT_W, (R + VT_H - 1) / VT_H, n_img), bv(64, 4);
+        dim3 gf((C + FT_W - 1) / FT_W, (R + FT_H - 1) / FT_H, n_img);
         if (o == 0) {
             Kern K0 = make_kern(py, 0);
             const int rows = p.upsample ? R / 2 : R, cols = p.upsample ? C / 2 : C;
-            if (p.upsample) VO_LAUNCH(k_base_h<true>, gh, bh, 0, s, src, rows, cols, R, C, b.tmp, py.tmp_plane, g.pitch, K0);
-            else VO_LAUNCH(k_base_h<false>, gh, bh, 0, s, src, rows, cols, R, C, b.tmp, py.tmp_plane, g.pitch, K0);
-            VO_LAUNCH(k_blur_v<false>, gv, bv, 0, s, b.tmp, py.tmp_plane, g.pitch, R, C, A + g.g_off[0],
-                               (const float*)nullptr, (float*)nullptr, g.plane, K0);
+            if (p.upsample) launch_blur<1>(gf, s, nullptr, g.plane, g.pitch, R, C, A + g.g_off[0], nullptr, K0, src, rows, cols);
+            else launch_blur<2>(gf, s, nullptr, g.plane, g.pitch, R, C, A + g.g_off[0], nullptr, K0, src, rows, cols);
         } else {
             const OctGeom& pg = py.oct[o - 1];
             size_t n = (size_t)n_img * R * C;
@@ -715,26 +1024,31 @@ void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_
             if (blocks > 4096) blocks = 4096;
             if (blocks < 1) blocks = 1;
             VO_LAUNCH(k_down, dim3(blocks), dim3(256), 0, s, A + pg.g_off[L], pg.plane, pg.pitch, A + g.g_off[0],
-                               g.plane, g.pitch, R, C, n_img);
+                      g.plane, g.pitch, R, C, n_img);
         }
         for (int i = 1; i < L + 3; ++i) {
             Kern K = make_kern(py, i);
-            VO_LAUNCH(k_blur_h, gh, bh, 0, s, A + g.g_off[i - 1], g.plane, g.pitch, R, C, b.tmp, py.tmp_plane, K);
-            VO_LAUNCH(k_blur_v<true>, gv, bv, 0, s, b.tmp, py.tmp_plane, g.pitch, R, C, A + g.g_off[i],
-                               A + g.g_off[i - 1], A + g.d_off[i - 1], g.plane, K);
+            launch_blur<0>(gf, s, A + g.g_off[i - 1], g.plane, g.pitch, R, C, A + g.g_off[i], A + g.d_off[i - 1], K, src, 0, 0);
         }
     }
     const float thr = (float)floor(0.5 * p.contrast_threshold / L * 255.0);
-    long words = (long)py.n_words * n_img;
-    int eb = (int)((words + 3) / 4);
-    if (eb > 8192) eb = 8192;
-    if (eb < 1) eb = 1;
-    VO_LAUNCH(k_ext_mask, dim3(eb), dim3(256), 0, s, d_py, A, b.mask, n_img, thr);
-    VO_LAUNCH(k_scan_words, dim3(n_img), dim3(1024), 0, s, b.mask, b.woff, b.n_cand, py.n_words);
-    int mb = (int)((words + 255) / 256);
-    if (mb > 4096) mb = 4096;
-    if (mb < 1) mb = 1;
-    VO_LAUNCH(k_emit, dim3(mb), dim3(256), 0, s, d_py, b.mask, b.woff, b.cand, b.cand_cap, n_img);
+    if (py.n_tiles > 0) {
+        int dev = 0, cus = 256;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const dim3 gt(std::min(py.n_tiles * n_img, 8 * cus));
+        switch (L) {
+        case 1: VO_LAUNCH(k_ext_tile<1>, gt, dim3(256), 0, s, d_py, A, b.mask, thr, n_img); break;
+        case 2: VO_LAUNCH(k_ext_tile<2>, gt, dim3(256), 0, s, d_py, A, b.mask, thr, n_img); break;
+        case 3: VO_LAUNCH(k_ext_tile<3>, gt, dim3(256), 0, s, d_py, A, b.mask, thr, n_img); break;
+        case 4: VO_LAUNCH(k_ext_tile<4>, gt, dim3(256), 0, s, d_py, A, b.mask, thr, n_img); break;
+        default: VO_LAUNCH(k_ext_tile<5>, gt, dim3(256), 0, s, d_py, A, b.mask, thr, n_img); break;
+        }
+    }
+    const dim3 gs(py.n_seg > 0 ? py.n_seg : 1, n_img);
+    VO_LAUNCH(k_seg_count, gs, dim3(256), 0, s, b.mask, b.woff, py.n_words, py.n_seg);
+    VO_LAUNCH(k_seg_scan, dim3(n_img), dim3(1024), 0, s, b.woff, b.n_cand, py.n_seg);
+    VO_LAUNCH(k_seg_emit, gs, dim3(256), 0, s, d_py, b.mask, (const uint32_t*)b.woff, b.cand, b.cand_cap);
     VO_LAUNCH(k_refine_orient, dim3(8192), dim3(64), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.cand_cap, n_img,
                        p.contrast_threshold, p.edge_threshold, p.sigma);
     VO_LAUNCH(k_scan_cands, dim3(n_img), dim3(1024), 0, s, b.cout, b.n_cand, b.koff, b.n_kp, b.cand_cap);

@@ -35,12 +35,14 @@ struct Profiler {
 };
 extern Profiler* g_prof;
 
-#define VO_LAUNCH(kernel, grid, block, shmem, stream, ...)                                  \
+#define VO_LAUNCH_NAMED(name, kernel, grid, block, shmem, stream, ...)                     \
     do {                                                                                   \
-        if (::vo::g_prof && ::vo::g_prof->on) ::vo::g_prof->begin(#kernel, stream);        \
+        if (::vo::g_prof && ::vo::g_prof->on) ::vo::g_prof->begin(name, stream);           \
         hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);               \
         if (::vo::g_prof && ::vo::g_prof->on) ::vo::g_prof->end(stream);                   \
     } while (0)
+#define VO_LAUNCH(kernel, grid, block, shmem, stream, ...) \
+    VO_LAUNCH_NAMED(#kernel, kernel, grid, block, shmem, stream, __VA_ARGS__)
 
 // ---------------------------------------------------------------------------
 // Scale-space arena.  For each octave o and level i, the planes of all images
@@ -68,7 +70,14 @@ struct Pyramid {
     int wbase[VO_SIFT_MAX_OCTAVES * 4 + 1];   // prefix over (o, layer-1) blocks; size n_oct*L+1
     int wrow[VO_SIFT_MAX_OCTAVES];            // words per row in octave o
     int n_words;                              // words per image
+    // extremum-test tiles (64 interior columns x 16 interior rows, all layers)
+    int tbase[VO_SIFT_MAX_OCTAVES + 1];       // prefix of tiles per octave
+    int n_tiles;                              // tiles per image
+    int n_seg;                                // 1024-word compaction segments per image
 };
+
+#define VO_EXT_TILE_ROWS 16
+#define VO_SEG_WORDS 1024
 
 // Packed candidate: c | r << 12 | layer << 24 | o << 27  (c, r < 4096)
 __host__ __device__ inline uint32_t pack_cand(int o, int layer, int r, int c) {
@@ -100,7 +109,7 @@ struct SiftBuffers {
     float* arena = nullptr;
     float* tmp = nullptr;              // horizontal-pass scratch [n_img][tmp_plane]
     unsigned long long* mask = nullptr;  // [n_img][n_words]
-    uint32_t* woff = nullptr;          // [n_img][n_words]
+    uint32_t* woff = nullptr;          // [n_img][n_seg] segment counts, then exclusive offsets
     uint32_t* cand = nullptr;          // [n_img][cand_cap]
     int* n_cand = nullptr;             // [n_img]  (uncapped count)
     CandOut* cout = nullptr;           // [n_img][cand_cap]

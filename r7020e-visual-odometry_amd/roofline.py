@@ -44,14 +44,12 @@ def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3) -> dict:
         out[name] = (b + nbytes, l + launches)
 
     R0, C0 = dims[0]
-    add("k_base_h<true>", n_img * (rows * cols + 4 * R0 * C0), 1)        # u8 in, fp32 row pass out
-    add("k_blur_v<false>", n_img * 8 * R0 * C0, 1)                        # row pass in, G0 out
+    add("k_blur_base", n_img * (rows * cols + 4 * R0 * C0), 1)           # u8 in (x2 upsample fused), G0 out
     for o, (R, C) in enumerate(dims):
         px = R * C * n_img
         if o:
             add("k_down", 8 * px, 1)                                      # 1 of 4 source px in, G0 out
-        add("k_blur_h", 8 * px * lv, lv)                                  # G_{i-1} in, row pass out
-        add("k_blur_v<true>", 16 * px * lv, lv)                           # row pass + G_{i-1} in, G_i + D_{i-1} out
+        add("k_blur_fused", 12 * px * lv, lv)                             # G_{i-1} in, G_i + D_{i-1} out
     # extremum test reads the L+2 DoG levels of every octave once
-    add("k_ext_mask", sum(4 * (layers + 2) * r * c for r, c in dims) * n_img, 1)
+    add(f"k_ext_tile<{layers}>", sum(4 * (layers + 2) * r * c for r, c in dims) * n_img, 1)
     return out
