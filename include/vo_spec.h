@@ -77,17 +77,22 @@ VO_HD float vo_expf(float x)
 /* ------------------------------------------------------------------------ */
 /* atan2 in DEGREES, result in [0, 360).  (OpenCV fastAtan2 convention:      */
 /* angle of the vector (x, y), counter-clockwise from +x.)  Accurate to      */
-/* ~1e-5 deg; only basic ops.                                                */
+/* ~1e-5 deg; only basic ops.  Written select-only with ONE division so the  */
+/* SIMT form has no divergent branches: with lo = min(|x|,|y|), hi = max,    */
+/*   t = lo/hi            if lo <= tan(pi/8)*hi  (tested as a float product) */
+/*   t = (lo-hi)/(lo+hi)  otherwise, and atan(lo/hi) = pi/4 + atan(t).       */
 /* ------------------------------------------------------------------------ */
-VO_HD float vo_atan_unit(float t)   /* atan(t) in radians for t in [0, 1] */
+VO_HD float vo_atan2_deg(float y, float x)
 {
-    float off = 0.0f;
-    if (t > 0.41421356f) {            /* atan(t) = pi/4 + atan((t-1)/(t+1)) */
-        t = (t - 1.0f) / (t + 1.0f);
-        off = 0.78539816339744831f;
-    }
-    float t2 = t * t;
-    /* odd Taylor series to t^17, |t| <= tan(pi/8) -> truncation < 2e-8 */
+    const float ax = fabsf(x), ay = fabsf(y);
+    const int swap = ay > ax;
+    const float lo = swap ? ax : ay, hi = swap ? ay : ax;
+    const int red = lo > 0.41421356f * hi;
+    const float num = red ? lo - hi : lo;
+    const float den = red ? lo + hi : hi;
+    const float t = num / (den > 0.0f ? den : 1.0f);      /* origin: num = 0 -> t = 0 */
+    const float t2 = t * t;
+    /* odd Taylor series to t^15, |t| <= tan(pi/8) -> truncation < 2e-8 */
     float p = -1.0f / 15.0f;
     p = fmaf(p, t2, 1.0f / 13.0f);
     p = fmaf(p, t2, -1.0f / 11.0f);
@@ -96,20 +101,11 @@ VO_HD float vo_atan_unit(float t)   /* atan(t) in radians for t in [0, 1] */
     p = fmaf(p, t2, 1.0f / 5.0f);
     p = fmaf(p, t2, -1.0f / 3.0f);
     p = p * t2;
-    return fmaf(p, t, t) + off;
-}
-
-VO_HD float vo_atan2_deg(float y, float x)
-{
-    float ax = fabsf(x), ay = fabsf(y);
-    float a;
-    if (ax == 0.0f && ay == 0.0f) return 0.0f;
-    if (ax >= ay) a = vo_atan_unit(ay / ax) * 57.295779513082321f;
-    else          a = 90.0f - vo_atan_unit(ax / ay) * 57.295779513082321f;
-    if (x < 0.0f) a = 180.0f - a;
-    if (y < 0.0f) a = 360.0f - a;
-    if (a >= 360.0f) a = 0.0f;
-    return a;
+    float a = (fmaf(p, t, t) + (red ? 0.78539816339744831f : 0.0f)) * 57.295779513082321f;
+    a = swap ? 90.0f - a : a;
+    a = x < 0.0f ? 180.0f - a : a;
+    a = y < 0.0f ? 360.0f - a : a;
+    return a >= 360.0f ? 0.0f : a;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -249,6 +245,16 @@ VO_HD uint32_t vo_rand_index(uint32_t r, uint32_t n) { return (uint32_t)(((uint6
 VO_HD int32_t vo_fx_quant(float v) { return (int32_t)rintf(v * VO_FX_SCALE); }
 VO_HD float vo_fx_to_float(int64_t s) { return (float)((double)s * (1.0 / 1048576.0)); }
 
+/* Descriptor histogram: unsigned 32-bit fixed point at 2^-10.  The gradient   */
+/* magnitude is pre-scaled by 2^10 (exact: a power of two), so each trilinear */
+/* share v >= 0 enters as rintf(v).  Overflow-free by construction: |dI| <=   */
+/* 255 so one share is < 361*2^10, and a spatial bin collects fewer than      */
+/* (2*hist_width+2)^2 <= 5.5e3 samples once the radius is capped at           */
+/* VO_SIFT_DESCR_RMAX (hist_width <= 36.3): < 2.1e9 < 2^32.                   */
+#define VO_DESC_FX_SCALE 1024.0f
+VO_HD uint32_t vo_desc_fx_quant(float v_scaled) { return (uint32_t)rintf(v_scaled); }
+VO_HD float vo_desc_fx_to_float(uint32_t s) { return (float)s * (1.0f / VO_DESC_FX_SCALE); }
+
 /* ------------------------------------------------------------------------ */
 /* SIFT scale-space constants (spec, OpenCV-4.x conventions).  Computed on  */
 /* the host by both the oracle and libvo with the deterministic exp/log     */
@@ -268,6 +274,7 @@ VO_HD float vo_fx_to_float(int64_t s) { return (float)((double)s * (1.0 / 104857
 #define VO_SIFT_DESCR_SCL 3.0f
 #define VO_SIFT_DESCR_MAG_THR 0.2f
 #define VO_SIFT_DESCR_INT_FCTR 512.0f
+#define VO_SIFT_DESCR_RMAX 128     /* descriptor window radius cap (38 at the defaults) */
 #define VO_SIFT_MAX_PEAKS 18      /* strict local maxima in a 36-bin circle */
 #define VO_FLT_EPSILON 1.19209290e-07f
 

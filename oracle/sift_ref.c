@@ -303,9 +303,10 @@ static void descriptor(const float* img, int rows, int cols, float xo, float yo,
     int radius = vo_round(hist_width * 1.4142135623730951f * (float)(d + 1) * 0.5f);
     int rmax = (int)sqrt((double)cols * cols + (double)rows * rows);
     if (radius > rmax) radius = rmax;
+    if (radius > VO_SIFT_DESCR_RMAX) radius = VO_SIFT_DESCR_RMAX;
     cos_t = cos_t / hist_width;
     sin_t = sin_t / hist_width;
-    int64_t hfx[(VO_SIFT_DESCR_W + 2) * (VO_SIFT_DESCR_W + 2) * (VO_SIFT_DESCR_BINS + 2)];
+    uint32_t hfx[(VO_SIFT_DESCR_W + 2) * (VO_SIFT_DESCR_W + 2) * (VO_SIFT_DESCR_BINS + 2)];
     memset(hfx, 0, sizeof(hfx));
     for (int i = -radius; i <= radius; ++i) {
         for (int j = -radius; j <= radius; ++j) {
@@ -320,7 +321,7 @@ static void descriptor(const float* img, int rows, int cols, float xo, float yo,
             float dy = AT(img, cols, r - 1, c) - AT(img, cols, r + 1, c);
             float w = vo_expf((c_rot * c_rot + r_rot * r_rot) * exp_scale);
             float ang = vo_atan2_deg(dy, dx);
-            float mag = sqrtf(dx * dx + dy * dy) * w;
+            float mag = (sqrtf(dx * dx + dy * dy) * w) * VO_DESC_FX_SCALE;   /* exact power-of-two pre-scale */
             float obin = (ang - ori) * bins_per_deg;
             int r0 = vo_floor(rbin), c0 = vo_floor(cbin), o0 = vo_floor(obin);
             rbin -= (float)r0; cbin -= (float)c0; obin -= (float)o0;
@@ -334,14 +335,14 @@ static void descriptor(const float* img, int rows, int cols, float xo, float yo,
             float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
             float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
             int idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
-            hfx[idx] += vo_fx_quant(v_rco000);
-            hfx[idx + 1] += vo_fx_quant(v_rco001);
-            hfx[idx + (n + 2)] += vo_fx_quant(v_rco010);
-            hfx[idx + (n + 3)] += vo_fx_quant(v_rco011);
-            hfx[idx + (d + 2) * (n + 2)] += vo_fx_quant(v_rco100);
-            hfx[idx + (d + 2) * (n + 2) + 1] += vo_fx_quant(v_rco101);
-            hfx[idx + (d + 3) * (n + 2)] += vo_fx_quant(v_rco110);
-            hfx[idx + (d + 3) * (n + 2) + 1] += vo_fx_quant(v_rco111);
+            hfx[idx] += vo_desc_fx_quant(v_rco000);
+            hfx[idx + 1] += vo_desc_fx_quant(v_rco001);
+            hfx[idx + (n + 2)] += vo_desc_fx_quant(v_rco010);
+            hfx[idx + (n + 3)] += vo_desc_fx_quant(v_rco011);
+            hfx[idx + (d + 2) * (n + 2)] += vo_desc_fx_quant(v_rco100);
+            hfx[idx + (d + 2) * (n + 2) + 1] += vo_desc_fx_quant(v_rco101);
+            hfx[idx + (d + 3) * (n + 2)] += vo_desc_fx_quant(v_rco110);
+            hfx[idx + (d + 3) * (n + 2) + 1] += vo_desc_fx_quant(v_rco111);
         }
     }
     float dst[VO_DESC_LEN];
@@ -350,7 +351,7 @@ static void descriptor(const float* img, int rows, int cols, float xo, float yo,
             int idx = ((i + 1) * (d + 2) + (j + 1)) * (n + 2);
             hfx[idx] += hfx[idx + n];
             hfx[idx + 1] += hfx[idx + n + 1];
-            for (int k = 0; k < n; ++k) dst[(i * d + j) * n + k] = vo_fx_to_float(hfx[idx + k]);
+            for (int k = 0; k < n; ++k) dst[(i * d + j) * n + k] = vo_desc_fx_to_float(hfx[idx + k]);
         }
     /* norms: pairwise tree 128 -> 1 (stride 64, 32, ..., 1) */
     float s[VO_DESC_LEN];

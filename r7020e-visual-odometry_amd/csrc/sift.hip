@@ -639,7 +639,7 @@ __global__ __launch_bounds__(64) void k_refine_orient(const Pyramid* __restrict_
     for (long t = blockIdx.x; t < total; t += gridDim.x) {
         int img, kidx;
         flat_item(n_cand, cand_cap, n_img, t, img, kidx);
-        const uint32_t pc = cand[(size_t)img * cand_cap + kidx];
+        const uint32_t pc = __builtin_amdgcn_readfirstlane(cand[(size_t)img * cand_cap + kidx]);   // wave-uniform -> scalar geometry loads
         const int c0 = pc & 4095, r0 = (pc >> 12) & 4095, layer0 = (pc >> 24) & 7, o = pc >> 27;
         const OctGeom& g = py->oct[o];
         const int rows = g.rows, cols = g.cols, P = g.pitch;
@@ -829,22 +829,30 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
 #define DW VO_SIFT_DESCR_W
 #define DN VO_SIFT_DESCR_BINS
 #define DHIST ((DW + 2) * (DW + 2) * (DN + 2))
+// Histogram copies: lane l adds into copy (l & (DCOPIES-1)), so neighbouring samples
+// (same cell, often the same orientation bin) no longer serialise on one LDS address.
+// Copy stride 360 dwords = 8 mod 32 banks.  u32 fixed point (vo_desc_fx_quant) sums
+// are order-free, so the copies are folded after the loop without changing a bit.
+#define DCOPIES 4
 
 __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                              const KpInt* __restrict__ kpi, const int* __restrict__ n_kp,
                                              uint8_t* __restrict__ desc, DescMeta* __restrict__ meta, int kp_cap, int n_img)
 {
-    __shared__ unsigned long long hfx[DHIST];
+    __shared__ uint32_t hfx[DCOPIES * DHIST];
+    __shared__ int rlo[2 * VO_SIFT_DESCR_RMAX + 2], rlen[2 * VO_SIFT_DESCR_RMAX + 2], rstart[2 * VO_SIFT_DESCR_RMAX + 3];
     const int lane = threadIdx.x;
     const long total = flat_total(n_kp, kp_cap, n_img);
     for (long t = blockIdx.x; t < total; t += gridDim.x) {
         int img, k;
         flat_item(n_kp, kp_cap, n_img, t, img, k);
-        const KpInt q = kpi[(size_t)img * kp_cap + k];
+        KpInt q = kpi[(size_t)img * kp_cap + k];
+        q.o = __builtin_amdgcn_readfirstlane(q.o);              // wave-uniform -> scalar geometry loads
+        q.layer = __builtin_amdgcn_readfirstlane(q.layer);
         const OctGeom& g = py->oct[q.o];
         const int rows = g.rows, cols = g.cols, P = g.pitch;
         const float* gim = arena + g.g_off[q.layer] + img * g.plane;
-        for (int b = lane; b < DHIST; b += 64) hfx[b] = 0ull;
+        for (int b = lane; b < DCOPIES * DHIST; b += 64) hfx[b] = 0u;
         float ori = 360.0f - q.angle;
         if (fabsf(ori - 360.0f) < VO_FLT_EPSILON) ori = 0.0f;
         const int px = vo_round(q.xo), pyy = vo_round(q.yo);
@@ -856,45 +864,109 @@ __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, con
         int radius = vo_round(hist_width * 1.4142135623730951f * (float)(DW + 1) * 0.5f);
         const int rmax = (int)sqrt((double)cols * cols + (double)rows * rows);
         if (radius > rmax) radius = rmax;
+        if (radius > VO_SIFT_DESCR_RMAX) radius = VO_SIFT_DESCR_RMAX;
         cos_t = cos_t / hist_width;
         sin_t = sin_t / hist_width;
+        // Only ~half of the (2r+1)^2 window lies inside the rotated 4x4-cell square.  Each
+        // window row i gets a conservative column interval [jlo, jhi] (a superset: +-2
+        // columns of margin over the real-arithmetic bounds, clamped to the image
+        // interior); rows are flattened with a prefix sum, and the exact float test below
+        // still decides every sample, so the histogram is unchanged (fixed-point sums are
+        // order-free) while the wave no longer idles through rejected samples.
+        const int nrows = 2 * radius + 1;
+        for (int rr = lane; rr < nrows; rr += 64) {
+            const int i = rr - radius, r = pyy + i;
+            int jlo = -radius, jhi = radius;
+            if (r <= 0 || r >= rows - 1) { jlo = 1; jhi = 0; }
+            else {
+                const double ct = cos_t, st = sin_t, fi = (double)i, lim = 0.5 * DW + 0.5 + 1e-3;   // rbin = r_rot + 1.5 in (-1, DW)
+                // |j*ct - i*st| < lim  and  |j*st + i*ct| < lim
+                if (fabs(ct) > 1e-9) {
+                    double a = (fi * st - lim) / ct, b = (fi * st + lim) / ct;
+                    if (a > b) { double t2 = a; a = b; b = t2; }
+                    jlo = max(jlo, (int)floor(a) - 2); jhi = min(jhi, (int)ceil(b) + 2);
+                } else if (fabs(fi * st) >= lim) { jlo = 1; jhi = 0; }
+                if (fabs(st) > 1e-9) {
+                    double a = (-fi * ct - lim) / st, b = (-fi * ct + lim) / st;
+                    if (a > b) { double t2 = a; a = b; b = t2; }
+                    jlo = max(jlo, (int)floor(a) - 2); jhi = min(jhi, (int)ceil(b) + 2);
+                } else if (fabs(fi * ct) >= lim) { jlo = 1; jhi = 0; }
+                jlo = max(jlo, 1 - px); jhi = min(jhi, cols - 2 - px);
+            }
+            rlo[rr] = jlo;
+            rlen[rr] = jhi >= jlo ? jhi - jlo + 1 : 0;
+        }
         __syncthreads();
-        const int side = 2 * radius + 1, nsamp = side * side;
-        for (int s = lane; s < nsamp; s += 64) {
-            const int i = s / side - radius, j = s - (s / side) * side - radius;
-            float c_rot = (float)j * cos_t - (float)i * sin_t;
-            float r_rot = (float)j * sin_t + (float)i * cos_t;
-            float rbin = r_rot + (float)(DW / 2) - 0.5f;
-            float cbin = c_rot + (float)(DW / 2) - 0.5f;
-            const int r = pyy + i, c = px + j;
-            if (!(rbin > -1.0f && rbin < (float)DW && cbin > -1.0f && cbin < (float)DW &&
-                  r > 0 && r < rows - 1 && c > 0 && c < cols - 1)) continue;
-            float dx = DAT(gim, P, r, c + 1) - DAT(gim, P, r, c - 1);
-            float dy = DAT(gim, P, r - 1, c) - DAT(gim, P, r + 1, c);
-            float w = vo_expf((c_rot * c_rot + r_rot * r_rot) * exp_scale);
-            float ang = vo_atan2_deg(dy, dx);
-            float mag = sqrtf(dx * dx + dy * dy) * w;
-            float obin = (ang - ori) * bins_per_deg;
-            int r0 = vo_floor(rbin), c0 = vo_floor(cbin), o0 = vo_floor(obin);
-            rbin -= (float)r0; cbin -= (float)c0; obin -= (float)o0;
-            if (o0 < 0) o0 += DN;
-            if (o0 >= DN) o0 -= DN;
-            float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-            float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
-            float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-            float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
-            float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
-            float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
-            float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-            const int idx = ((r0 + 1) * (DW + 2) + c0 + 1) * (DN + 2) + o0;
-            atomicAdd(&hfx[idx], (unsigned long long)(long long)vo_fx_quant(v_rco000));
-            atomicAdd(&hfx[idx + 1], (unsigned long long)(long long)vo_fx_quant(v_rco001));
-            atomicAdd(&hfx[idx + (DN + 2)], (unsigned long long)(long long)vo_fx_quant(v_rco010));
-            atomicAdd(&hfx[idx + (DN + 3)], (unsigned long long)(long long)vo_fx_quant(v_rco011));
-            atomicAdd(&hfx[idx + (DW + 2) * (DN + 2)], (unsigned long long)(long long)vo_fx_quant(v_rco100));
-            atomicAdd(&hfx[idx + (DW + 2) * (DN + 2) + 1], (unsigned long long)(long long)vo_fx_quant(v_rco101));
-            atomicAdd(&hfx[idx + (DW + 3) * (DN + 2)], (unsigned long long)(long long)vo_fx_quant(v_rco110));
-            atomicAdd(&hfx[idx + (DW + 3) * (DN + 2) + 1], (unsigned long long)(long long)vo_fx_quant(v_rco111));
+        {   // wave-parallel exclusive prefix over the rows (<= 2*RMAX+1): lane owns a chunk of rows
+            const int per = (nrows + 63) >> 6, r0w = lane * per;
+            int sum = 0;
+            for (int q = 0; q < per; ++q) if (r0w + q < nrows) sum += rlen[r0w + q];
+            int inc = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(inc, o); if (lane >= o) inc += y; }
+            int acc = inc - sum;
+            for (int q = 0; q < per; ++q) if (r0w + q < nrows) { rstart[r0w + q] = acc; acc += rlen[r0w + q]; }
+            if (lane == 63) rstart[nrows] = inc;
+        }
+        __syncthreads();
+        const int nsamp = rstart[nrows];
+        uint32_t* hc = hfx + (lane & (DCOPIES - 1)) * DHIST;
+        int lo = 0;                                      // current row; s only grows, so advance
+        constexpr int U = 4;                             // samples per lane per iteration: 16 loads in flight
+        for (int s0 = lane; s0 < nsamp; s0 += 64 * U) {
+            float crot[U], rrot[U], gdx[U], gdy[U];
+            bool ok[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {                // phase 1: indices, exact validity test, gradient loads
+                const int s = s0 + 64 * u;
+                ok[u] = false; crot[u] = 0.0f; rrot[u] = 0.0f; gdx[u] = 0.0f; gdy[u] = 0.0f;
+                if (s < nsamp) {
+                    while (rstart[lo + 1] <= s) ++lo;
+                    const int i = lo - radius, j = rlo[lo] + (s - rstart[lo]);
+                    const float c_rot = (float)j * cos_t - (float)i * sin_t;
+                    const float r_rot = (float)j * sin_t + (float)i * cos_t;
+                    const float rbin = r_rot + (float)(DW / 2) - 0.5f;
+                    const float cbin = c_rot + (float)(DW / 2) - 0.5f;
+                    const int r = pyy + i, c = px + j;
+                    if (rbin > -1.0f && rbin < (float)DW && cbin > -1.0f && cbin < (float)DW &&
+                        r > 0 && r < rows - 1 && c > 0 && c < cols - 1) {
+                        ok[u] = true; crot[u] = c_rot; rrot[u] = r_rot;
+                        gdx[u] = DAT(gim, P, r, c + 1) - DAT(gim, P, r, c - 1);
+                        gdy[u] = DAT(gim, P, r - 1, c) - DAT(gim, P, r + 1, c);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {                // phase 2: weights, bins, fixed-point LDS atomics
+                if (!ok[u]) continue;
+                const float c_rot = crot[u], r_rot = rrot[u], dx = gdx[u], dy = gdy[u];
+                float rbin = r_rot + (float)(DW / 2) - 0.5f;
+                float cbin = c_rot + (float)(DW / 2) - 0.5f;
+                float w = vo_expf((c_rot * c_rot + r_rot * r_rot) * exp_scale);
+                float ang = vo_atan2_deg(dy, dx);
+                float mag = (sqrtf(dx * dx + dy * dy) * w) * VO_DESC_FX_SCALE;
+                float obin = (ang - ori) * bins_per_deg;
+                int r0 = vo_floor(rbin), c0 = vo_floor(cbin), o0 = vo_floor(obin);
+                rbin -= (float)r0; cbin -= (float)c0; obin -= (float)o0;
+                if (o0 < 0) o0 += DN;
+                if (o0 >= DN) o0 -= DN;
+                float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+                float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+                float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+                float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+                float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+                float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+                float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+                uint32_t* h = hc + ((r0 + 1) * (DW + 2) + c0 + 1) * (DN + 2) + o0;
+                atomicAdd(h, vo_desc_fx_quant(v_rco000));
+                atomicAdd(h + 1, vo_desc_fx_quant(v_rco001));
+                atomicAdd(h + (DN + 2), vo_desc_fx_quant(v_rco010));
+                atomicAdd(h + (DN + 3), vo_desc_fx_quant(v_rco011));
+                atomicAdd(h + (DW + 2) * (DN + 2), vo_desc_fx_quant(v_rco100));
+                atomicAdd(h + (DW + 2) * (DN + 2) + 1, vo_desc_fx_quant(v_rco101));
+                atomicAdd(h + (DW + 3) * (DN + 2), vo_desc_fx_quant(v_rco110));
+                atomicAdd(h + (DW + 3) * (DN + 2) + 1, vo_desc_fx_quant(v_rco111));
+            }
         }
         __syncthreads();
         // fold the circular orientation bins and convert; lane holds dst[lane], dst[lane+64]
@@ -905,9 +977,13 @@ __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, con
             const int cell = kk / DN, ob = kk - cell * DN;
             const int ci = cell / DW, cj = cell - ci * DW;
             const int base = ((ci + 1) * (DW + 2) + (cj + 1)) * (DN + 2);
-            long long v = (long long)hfx[base + ob];
-            if (ob < 2) v += (long long)hfx[base + DN + ob];
-            dv[h] = vo_fx_to_float((int64_t)v);
+            uint32_t v = 0;
+#pragma unroll
+            for (int cp = 0; cp < DCOPIES; ++cp) {
+                v += hfx[cp * DHIST + base + ob];
+                if (ob < 2) v += hfx[cp * DHIST + base + DN + ob];
+            }
+            dv[h] = vo_desc_fx_to_float(v);
         }
         float s = dv[0] * dv[0] + dv[1] * dv[1];
 #pragma unroll
