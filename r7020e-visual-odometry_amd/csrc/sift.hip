@@ -17,9 +17,12 @@
 //                         (fixed-point LDS atomics), norms as a wave tree
 // Every float expression follows oracle/sift_ref.c operation for operation.
 #include "vo_internal.h"
+#include <cstdlib>
 #include <cstring>
 #include <cmath>
 #include <algorithm>
+#include <utility>
+#include <type_traits>
 
 namespace vo {
 
@@ -42,7 +45,7 @@ void build_pyramid_geometry(Pyramid& py, int rows, int cols, int n_img, const vo
         OctGeom& g = py.oct[o];
         if (o) { R /= 2; C /= 2; }
         g.rows = R; g.cols = C;
-        g.pitch = (C + 63) / 64 * 64;
+        g.pitch = (C + 255) / 256 * 256;    // whole 256-column blur strips: masked-off lanes store into padding
         g.plane = (size_t)g.rows * g.pitch;
         for (int i = 0; i < L + 3; ++i) { g.g_off[i] = off; off += g.plane * n_img; }
         for (int i = 0; i < L + 2; ++i) { g.d_off[i] = off; off += g.plane * n_img; }
@@ -333,6 +336,184 @@ __global__ __launch_bounds__(256) void k_blur_pipe(const float* __restrict__ src
         }
         __syncthreads();
     }
+}
+
+// ---------------------------------------------------------------------------
+// Streaming level blur (MODE 0, compiled radius): one wave per (image, band of
+// TH output rows, strip of 256 columns).  The wave walks the band's TH + 2r
+// input rows top to bottom; each lane owns 4 consecutive columns.
+//   - input rows are prefetched P rows ahead into registers (one 16-B load per
+//     lane plus the 2*R4 halo floats), staged through a one-row LDS buffer for
+//     the horizontal pass (the only cross-lane exchange);
+//   - the horizontal results of the last RS >= 2r+1 rows live in a register
+//     ring; steps are generated at compile time (vo_static_for) so every ring
+//     and prefetch index is a constant; the vertical pass runs on float2 column
+//     pairs (packed v_pk_* math, IEEE per element);
+//   - G_i and D_{i-1} = G_i - G_{i-1} are stored as 16-B row segments; the
+//     G_{i-1} row for D is re-loaded P rows ahead (an L2 hit).
+// The steady-state loop issues the same memory operations on every path (no
+// conditional loads or stores: rows past the band are valid reflected rows,
+// masked-off columns store into the row's padding column), so the compiler's
+// s_waitcnt counting keeps P rows of loads in flight instead of draining.
+// TH is a multiple of RS; the last band is shifted up to end at row R (rows
+// computed twice are bit-identical).  Arithmetic per output is exactly
+// k_blur_fused's (row pass, then column pass, same order).
+// ---------------------------------------------------------------------------
+typedef float vo_f2 __attribute__((ext_vector_type(2)));
+typedef float vo_f4 __attribute__((ext_vector_type(4)));
+
+// compile-time loop: f(std::integral_constant<int, 0>) ... f(<N-1>), so array
+// indices derived from the counter are constants (register-resident rings)
+template <typename F, int... I>
+__device__ __forceinline__ void vo_static_for_impl(F&& f, std::integer_sequence<int, I...>)
+{
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void vo_static_for(F&& f) { vo_static_for_impl(f, std::make_integer_sequence<int, N>{}); }
+
+__device__ inline int xcd_remap(int bid, int n)
+{
+    // consecutive logical ids on the same XCD (blocks are dealt round-robin over 8 XCDs)
+    const int q = n >> 3, rm = n & 7, xcd = bid & 7, idx = bid >> 3;
+    return xcd < rm ? xcd * (q + 1) + idx : rm * (q + 1) + (xcd - rm) * q + idx;
+}
+
+#define BS_W 256          // strip width (64 lanes x 4 columns)
+#define BS_P 4            // prefetch depth (rows)
+__host__ __device__ constexpr int bs_r4(int r) { return (r + 3) & ~3; }
+__host__ __device__ constexpr int bs_rw(int r) { return BS_W + 2 * bs_r4(r); }
+
+template <int RAD, bool EDGE>
+__device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, int pitch, int R, int C,
+                                                 float* __restrict__ g_out, float* __restrict__ d_out, const Kern& K,
+                                                 int x0, int y0, int TH, float* rb)
+{
+    constexpr int P = BS_P;                                // prefetch depth = steps per loop block
+    constexpr int R4 = bs_r4(RAD);                         // halo rounded to whole float4s
+    constexpr int NQ = 1 + R4 / 2;                         // float4 reads per lane window
+    constexpr int NR = 2 * RAD + P;                        // ring: 2r carried rows + P new per block
+    constexpr int F = (2 * RAD + P - 1) / P * P;           // ring-fill steps (no output)
+    constexpr int E = F - 2 * RAD;                         // extra rows read above the band
+    constexpr int RW = bs_rw(RAD);                         // staged row floats (one LDS ring slot)
+    constexpr int NSLOT = RAD + 1;                         // staged rows kept: D needs the row of step kk-r
+    const int lane = threadIdx.x;
+    const int xl = x0 + 4 * lane;
+    // halo lanes: [0, R4/4) left, [R4/4, R4/2) right.  The others load lane 0's
+    // segment (same cache line) and stage it into a private dummy LDS slot, so
+    // every lane issues the same instructions.
+    const bool hl = lane < R4 / 4, hr = !hl && lane < R4 / 2;
+    const int hx = hl ? x0 - R4 + 4 * lane : hr ? x0 + BS_W + 4 * (lane - R4 / 4) : x0 - R4;
+    const int hpos = hl ? 4 * lane : hr ? R4 + BS_W + 4 * (lane - R4 / 4) : -1;
+    float* const dummy = rb + NSLOT * RW + 4 * lane;
+    int cm[4], ch[4];                                      // border strips: reflect-101 source columns
+    if (EDGE) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            cm[i] = vo_reflect101(xl + i, C);
+            ch[i] = vo_reflect101(hx + i, C);
+        }
+    }
+    float k[RAD + 1];
+#pragma unroll
+    for (int j = 0; j <= RAD; ++j) k[j] = K.k[j];
+
+    vo_f4 pf[P], ph[P];
+    vo_f2 H[NR][2];
+
+    // loads for step kk into prefetch slot SL: input row y0-r-E+kk (reflected)
+#define VO_BS_LOAD(KK, SL)                                                                        \
+    do {                                                                                          \
+        const float* rowp_ = sp + (size_t)vo_reflect101(y0 - RAD - E + (KK), R) * pitch;          \
+        if (!EDGE) {                                                                              \
+            pf[SL] = *reinterpret_cast<const vo_f4*>(rowp_ + xl);                                 \
+            ph[SL] = *reinterpret_cast<const vo_f4*>(rowp_ + hx);                                 \
+        } else {                                                                                  \
+            pf[SL] = vo_f4{rowp_[cm[0]], rowp_[cm[1]], rowp_[cm[2]], rowp_[cm[3]]};               \
+            ph[SL] = vo_f4{rowp_[ch[0]], rowp_[ch[1]], rowp_[ch[2]], rowp_[ch[3]]};               \
+        }                                                                                         \
+    } while (0)
+
+    // P steps kk0 .. kk0+P-1: stage input row kk into LDS slot kk % NSLOT, prefetch
+    // row kk+P, horizontal pass into ring slot 2r+u, and (STORE) the vertical pass
+    // over ring slots u .. u+2r for output row y0 + kk - F, whose G_{i-1} is the row
+    // staged r steps earlier; then the ring shifts down by P.
+    int slot = 0;                                          // kk % NSLOT, carried
+    auto block = [&](int kk0, auto store_c) {
+        vo_static_for<P>([&](auto uc) {
+            constexpr int u = decltype(uc)::value;
+            const int kk = kk0 + u;
+            float* const row = rb + slot * RW;
+            *reinterpret_cast<vo_f4*>(row + R4 + 4 * lane) = pf[u];
+            *reinterpret_cast<vo_f4*>(hpos >= 0 ? row + hpos : dummy) = ph[u];
+            __syncthreads();                              // one-wave block: orders the LDS rows only
+            VO_BS_LOAD(kk + P, u);
+            float w[4 * NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const vo_f4 t = *reinterpret_cast<const vo_f4*>(row + 4 * lane + 4 * q);
+                w[4 * q] = t.x; w[4 * q + 1] = t.y; w[4 * q + 2] = t.z; w[4 * q + 3] = t.w;
+            }
+            float h[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float acc = k[0] * w[R4 + i];
+#pragma unroll
+                for (int j = 1; j <= RAD; ++j) acc = fmaf(k[j], w[R4 + i - j] + w[R4 + i + j], acc);
+                h[i] = acc;
+            }
+            H[2 * RAD + u][0] = vo_f2{h[0], h[1]};
+            H[2 * RAD + u][1] = vo_f2{h[2], h[3]};
+            if constexpr (decltype(store_c)::value) {
+                const int ps = slot >= RAD ? slot - RAD : slot + 1;        // (kk - r) % NSLOT
+                const vo_f4 gp = *reinterpret_cast<const vo_f4*>(rb + ps * RW + R4 + 4 * lane);
+                vo_f2 o[2];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    vo_f2 acc = vo_f2{k[0], k[0]} * H[u + RAD][c];
+#pragma unroll
+                    for (int j = 1; j <= RAD; ++j)
+                        acc = __builtin_elementwise_fma(vo_f2{k[j], k[j]}, H[u + RAD - j][c] + H[u + RAD + j][c], acc);
+                    o[c] = acc;
+                }
+                const vo_f4 g4 = vo_f4{o[0].x, o[0].y, o[1].x, o[1].y};
+                const vo_f4 d4 = g4 - gp;
+                // columns >= C land in the row padding (pitch is a whole number of strips)
+                const size_t off = (size_t)(y0 + kk - F) * pitch + xl;
+                __builtin_nontemporal_store(g4, reinterpret_cast<vo_f4*>(g_out + off));
+                __builtin_nontemporal_store(d4, reinterpret_cast<vo_f4*>(d_out + off));
+            }
+            __syncthreads();
+            slot = slot == RAD ? 0 : slot + 1;
+        });
+#pragma unroll
+        for (int q = 0; q < 2 * RAD; ++q) { H[q][0] = H[q + P][0]; H[q][1] = H[q + P][1]; }
+    };
+
+    vo_static_for<P>([&](auto uc) { VO_BS_LOAD(decltype(uc)::value, decltype(uc)::value); });
+#pragma unroll 1
+    for (int kk0 = 0; kk0 < F; kk0 += P) block(kk0, std::false_type{});          // ring fill
+#pragma unroll 1
+    for (int kk0 = F; kk0 < F + TH; kk0 += P) block(kk0, std::true_type{});      // TH % P == 0
+#undef VO_BS_LOAD
+}
+
+template <int RAD>
+__global__ __launch_bounds__(64, RAD <= 6 ? 3 : 2) void k_blur_stream(const float* __restrict__ src, size_t plane, int pitch, int R, int C,
+                                                    float* __restrict__ g_out, float* __restrict__ d_out, Kern K,
+                                                    int n_strips, int n_bands, int TH)
+{
+    constexpr int R4 = bs_r4(RAD);
+    extern __shared__ __attribute__((aligned(16))) float rb[];   // (r+1) staged rows + per-lane dummy halo slots
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int strip = bid % n_strips, tb = bid / n_strips;
+    const int band = tb % n_bands, img = tb / n_bands;
+    const int x0 = strip * BS_W, y0 = min(band * TH, R - TH);
+    const size_t ob = img * plane;
+    if (x0 - R4 < 0 || x0 + BS_W + R4 > C)
+        blur_stream_body<RAD, true>(src + ob, pitch, R, C, g_out + ob, d_out + ob, K, x0, y0, TH, rb);
+    else
+        blur_stream_body<RAD, false>(src + ob, pitch, R, C, g_out + ob, d_out + ob, K, x0, y0, TH, rb);
 }
 
 // next octave base.  grid over outputs
@@ -1036,6 +1217,19 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
                           float* d, const Kern& K, const ImageSrc& isrc, int in_rows, int in_cols)
 {
     const size_t lds = sizeof(float) * ft_lds_floats(K.r);
+    static const int use_pipe = getenv("VO_BLUR_PIPE") ? atoi(getenv("VO_BLUR_PIPE")) : 0;
+    if constexpr (MODE == 0 && RAD > 0) if (!use_pipe) {
+        static const int th_env = getenv("VO_BLUR_TH") ? atoi(getenv("VO_BLUR_TH")) : 48;
+        const int TH = std::max(BS_P, th_env / BS_P * BS_P);       // band height: a multiple of P
+        if (R >= TH) {
+            const int n_strips = (C + BS_W - 1) / BS_W, n_bands = (R + TH - 1) / TH;
+            const int blocks = n_strips * n_bands * (int)grid.z;
+            const size_t lds = sizeof(float) * ((RAD + 1) * bs_rw(RAD) + 256);
+            VO_LAUNCH_NAMED("k_blur_fused", k_blur_stream<RAD>, dim3(blocks), dim3(64), lds, s, src, plane, pitch, R, C, g,
+                            d, K, n_strips, n_bands, TH);
+            return;
+        }
+    }
     if (MODE == 0 && RAD > 0) {
         // persistent grid: as many blocks as can be co-resident, walking all tiles
         static int per_cu = 0;
