@@ -48,7 +48,6 @@ void build_pyramid_geometry(Pyramid& py, int rows, int cols, int n_img, const vo
         g.pitch = (C + 255) / 256 * 256;    // whole 256-column blur strips: masked-off lanes store into padding
         g.plane = (size_t)g.rows * g.pitch;
         for (int i = 0; i < L + 3; ++i) { g.g_off[i] = off; off += g.plane * n_img; }
-        for (int i = 0; i < L + 2; ++i) { g.d_off[i] = off; off += g.plane * n_img; }
         if (g.plane > tmp_plane) tmp_plane = g.plane;
     }
     py.total = off;
@@ -234,7 +233,7 @@ __global__ __launch_bounds__(256) void k_blur_fused(const float* __restrict__ sr
                 if (y < R) {
                     const size_t o = img * plane + (size_t)y * pitch + x;
                     g_out[o] = out[i];
-                    if (MODE == 0) d_out[o] = out[i] - in[(y0l + i + r) * IW + c + r];
+                    if (MODE == 0 && d_out) d_out[o] = out[i] - in[(y0l + i + r) * IW + c + r];
                 }
             }
         }
@@ -329,7 +328,7 @@ __global__ __launch_bounds__(256) void k_blur_pipe(const float* __restrict__ src
                     if (y < R) {
                         const size_t o = img * plane + (size_t)y * pitch + x;
                         g_out[o] = acc;
-                        d_out[o] = acc - in[(y0l + i + RAD) * IW + c + RAD];
+                        if (d_out) d_out[o] = acc - in[(y0l + i + RAD) * IW + c + RAD];
                     }
                 }
             }
@@ -349,8 +348,9 @@ __global__ __launch_bounds__(256) void k_blur_pipe(const float* __restrict__ src
 //     ring; steps are generated at compile time (vo_static_for) so every ring
 //     and prefetch index is a constant; the vertical pass runs on float2 column
 //     pairs (packed v_pk_* math, IEEE per element);
-//   - G_i and D_{i-1} = G_i - G_{i-1} are stored as 16-B row segments; the
-//     G_{i-1} row for D is re-loaded P rows ahead (an L2 hit).
+//   - G_i is stored as 16-B non-temporal row segments.  DoG planes are never
+//     materialised: D_{i-1} = G_i - G_{i-1} is formed where it is consumed
+//     (extremum test, refinement), the same float subtraction.
 // The steady-state loop issues the same memory operations on every path (no
 // conditional loads or stores: rows past the band are valid reflected rows,
 // masked-off columns store into the row's padding column), so the compiler's
@@ -386,7 +386,7 @@ __host__ __device__ constexpr int bs_rw(int r) { return BS_W + 2 * bs_r4(r); }
 
 template <int RAD, bool EDGE>
 __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, int pitch, int R, int C,
-                                                 float* __restrict__ g_out, float* __restrict__ d_out, const Kern& K,
+                                                 float* __restrict__ g_out, const Kern& K,
                                                  int x0, int y0, int TH, float* rb)
 {
     constexpr int P = BS_P;                                // prefetch depth = steps per loop block
@@ -396,7 +396,6 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
     constexpr int F = (2 * RAD + P - 1) / P * P;           // ring-fill steps (no output)
     constexpr int E = F - 2 * RAD;                         // extra rows read above the band
     constexpr int RW = bs_rw(RAD);                         // staged row floats (one LDS ring slot)
-    constexpr int NSLOT = RAD + 1;                         // staged rows kept: D needs the row of step kk-r
     const int lane = threadIdx.x;
     const int xl = x0 + 4 * lane;
     // halo lanes: [0, R4/4) left, [R4/4, R4/2) right.  The others load lane 0's
@@ -405,7 +404,7 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
     const bool hl = lane < R4 / 4, hr = !hl && lane < R4 / 2;
     const int hx = hl ? x0 - R4 + 4 * lane : hr ? x0 + BS_W + 4 * (lane - R4 / 4) : x0 - R4;
     const int hpos = hl ? 4 * lane : hr ? R4 + BS_W + 4 * (lane - R4 / 4) : -1;
-    float* const dummy = rb + NSLOT * RW + 4 * lane;
+    float* const dummy = rb + RW + 4 * lane;
     int cm[4], ch[4];                                      // border strips: reflect-101 source columns
     if (EDGE) {
 #pragma unroll
@@ -434,16 +433,14 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
         }                                                                                         \
     } while (0)
 
-    // P steps kk0 .. kk0+P-1: stage input row kk into LDS slot kk % NSLOT, prefetch
-    // row kk+P, horizontal pass into ring slot 2r+u, and (STORE) the vertical pass
-    // over ring slots u .. u+2r for output row y0 + kk - F, whose G_{i-1} is the row
-    // staged r steps earlier; then the ring shifts down by P.
-    int slot = 0;                                          // kk % NSLOT, carried
+    // P steps kk0 .. kk0+P-1: stage input row kk into LDS, prefetch row kk+P,
+    // horizontal pass into ring slot 2r+u, and (STORE) the vertical pass over ring
+    // slots u .. u+2r for output row y0 + kk - F; then the ring shifts down by P.
     auto block = [&](int kk0, auto store_c) {
         vo_static_for<P>([&](auto uc) {
             constexpr int u = decltype(uc)::value;
             const int kk = kk0 + u;
-            float* const row = rb + slot * RW;
+            float* const row = rb;
             *reinterpret_cast<vo_f4*>(row + R4 + 4 * lane) = pf[u];
             *reinterpret_cast<vo_f4*>(hpos >= 0 ? row + hpos : dummy) = ph[u];
             __syncthreads();                              // one-wave block: orders the LDS rows only
@@ -465,8 +462,6 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
             H[2 * RAD + u][0] = vo_f2{h[0], h[1]};
             H[2 * RAD + u][1] = vo_f2{h[2], h[3]};
             if constexpr (decltype(store_c)::value) {
-                const int ps = slot >= RAD ? slot - RAD : slot + 1;        // (kk - r) % NSLOT
-                const vo_f4 gp = *reinterpret_cast<const vo_f4*>(rb + ps * RW + R4 + 4 * lane);
                 vo_f2 o[2];
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
@@ -477,14 +472,11 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                     o[c] = acc;
                 }
                 const vo_f4 g4 = vo_f4{o[0].x, o[0].y, o[1].x, o[1].y};
-                const vo_f4 d4 = g4 - gp;
                 // columns >= C land in the row padding (pitch is a whole number of strips)
                 const size_t off = (size_t)(y0 + kk - F) * pitch + xl;
                 __builtin_nontemporal_store(g4, reinterpret_cast<vo_f4*>(g_out + off));
-                __builtin_nontemporal_store(d4, reinterpret_cast<vo_f4*>(d_out + off));
             }
             __syncthreads();
-            slot = slot == RAD ? 0 : slot + 1;
         });
 #pragma unroll
         for (int q = 0; q < 2 * RAD; ++q) { H[q][0] = H[q + P][0]; H[q][1] = H[q + P][1]; }
@@ -500,20 +492,19 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
 
 template <int RAD>
 __global__ __launch_bounds__(64, RAD <= 6 ? 3 : 2) void k_blur_stream(const float* __restrict__ src, size_t plane, int pitch, int R, int C,
-                                                    float* __restrict__ g_out, float* __restrict__ d_out, Kern K,
-                                                    int n_strips, int n_bands, int TH)
+                                                    float* __restrict__ g_out, Kern K, int n_strips, int n_bands, int TH)
 {
     constexpr int R4 = bs_r4(RAD);
-    extern __shared__ __attribute__((aligned(16))) float rb[];   // (r+1) staged rows + per-lane dummy halo slots
+    __shared__ __attribute__((aligned(16))) float rb[bs_rw(RAD) + 256];   // staged row + per-lane dummy halo slots
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int strip = bid % n_strips, tb = bid / n_strips;
     const int band = tb % n_bands, img = tb / n_bands;
     const int x0 = strip * BS_W, y0 = min(band * TH, R - TH);
     const size_t ob = img * plane;
     if (x0 - R4 < 0 || x0 + BS_W + R4 > C)
-        blur_stream_body<RAD, true>(src + ob, pitch, R, C, g_out + ob, d_out + ob, K, x0, y0, TH, rb);
+        blur_stream_body<RAD, true>(src + ob, pitch, R, C, g_out + ob, K, x0, y0, TH, rb);
     else
-        blur_stream_body<RAD, false>(src + ob, pitch, R, C, g_out + ob, d_out + ob, K, x0, y0, TH, rb);
+        blur_stream_body<RAD, false>(src + ob, pitch, R, C, g_out + ob, K, x0, y0, TH, rb);
 }
 
 // next octave base.  grid over outputs
@@ -591,22 +582,22 @@ __global__ __launch_bounds__(256) void k_ext_tile(const Pyramid* __restrict__ py
                 const int rr = e / (ET_W + 2), cc = e - rr * (ET_W + 2);
                 off[q] = min(r0 - 1 + rr, g.rows - 1) * g.pitch + min(c0 - 1 + cc, g.cols - 1);
             }
-            float tv[L + 2][PQ];
+            float tv[L + 3][PQ];                          // Gaussian levels 0 .. L+2
 #pragma unroll
-            for (int lv = 0; lv < L + 2; ++lv) {
-                const float* pl = arena + g.d_off[lv] + img * g.plane;
+            for (int lv = 0; lv < L + 3; ++lv) {
+                const float* pl = arena + g.g_off[lv] + img * g.plane;
 #pragma unroll
                 for (int q = 0; q < PQ; ++q)
                     if (tid + 256 * q < PE) tv[lv][q] = pl[off[q]];
             }
 #pragma unroll
-            for (int lv = 0; lv < L + 2; ++lv)
+            for (int lv = 0; lv < L + 2; ++lv)            // D_lv = G_{lv+1} - G_lv
 #pragma unroll
                 for (int q = 0; q < PQ; ++q) {
                     const int e = tid + 256 * q;
                     if (e < PE) {
                         const int rr = e / (ET_W + 2), cc = e - rr * (ET_W + 2);
-                        lds[(lv * ET_LR + rr) * ET_LW + cc] = tv[lv][q];
+                        lds[(lv * ET_LR + rr) * ET_LW + cc] = tv[lv + 1][q] - tv[lv][q];
                     }
                 }
         }
@@ -824,6 +815,8 @@ __global__ __launch_bounds__(64) void k_refine_orient(const Pyramid* __restrict_
         const int c0 = pc & 4095, r0 = (pc >> 12) & 4095, layer0 = (pc >> 24) & 7, o = pc >> 27;
         const OctGeom& g = py->oct[o];
         const int rows = g.rows, cols = g.cols, P = g.pitch;
+        const size_t lstride = g.g_off[1] - g.g_off[0];    // next Gaussian level of the same image
+#define DOGV(p, P, y, x) (DAT((p) + lstride, P, y, x) - DAT(p, P, y, x))
         CandOut* out = cout + (size_t)img * cand_cap + kidx;
         // ---- adjustLocalExtrema (wave-uniform) ----
         const float img_scale = 1.0f / 255.0f;
@@ -833,19 +826,20 @@ __global__ __launch_bounds__(64) void k_refine_orient(const Pyramid* __restrict_
         int it = 0;
         bool ok = true;
         for (; it < VO_SIFT_MAX_INTERP; ++it) {
-            const float* im = arena + g.d_off[layer] + img * g.plane;
-            const float* pv = arena + g.d_off[layer - 1] + img * g.plane;
-            const float* nx = arena + g.d_off[layer + 1] + img * g.plane;
-            float dD[3] = {(DAT(im, P, r, c + 1) - DAT(im, P, r, c - 1)) * ds,
-                           (DAT(im, P, r + 1, c) - DAT(im, P, r - 1, c)) * ds,
-                           (DAT(nx, P, r, c) - DAT(pv, P, r, c)) * ds};
-            float v2 = DAT(im, P, r, c) * 2.0f;
-            float dxx = (DAT(im, P, r, c + 1) + DAT(im, P, r, c - 1) - v2) * ss;
-            float dyy = (DAT(im, P, r + 1, c) + DAT(im, P, r - 1, c) - v2) * ss;
-            float dss = (DAT(nx, P, r, c) + DAT(pv, P, r, c) - v2) * ss;
-            float dxy = (DAT(im, P, r + 1, c + 1) - DAT(im, P, r + 1, c - 1) - DAT(im, P, r - 1, c + 1) + DAT(im, P, r - 1, c - 1)) * cs;
-            float dxs = (DAT(nx, P, r, c + 1) - DAT(nx, P, r, c - 1) - DAT(pv, P, r, c + 1) + DAT(pv, P, r, c - 1)) * cs;
-            float dys = (DAT(nx, P, r + 1, c) - DAT(nx, P, r - 1, c) - DAT(pv, P, r + 1, c) + DAT(pv, P, r - 1, c)) * cs;
+            const float* gb = arena + img * g.plane;
+            const float* im = gb + g.g_off[layer];          // DoG level l = G_{l+1} - G_l (VO_DOG)
+            const float* pv = gb + g.g_off[layer - 1];
+            const float* nx = gb + g.g_off[layer + 1];
+            float dD[3] = {(DOGV(im, P, r, c + 1) - DOGV(im, P, r, c - 1)) * ds,
+                           (DOGV(im, P, r + 1, c) - DOGV(im, P, r - 1, c)) * ds,
+                           (DOGV(nx, P, r, c) - DOGV(pv, P, r, c)) * ds};
+            float v2 = DOGV(im, P, r, c) * 2.0f;
+            float dxx = (DOGV(im, P, r, c + 1) + DOGV(im, P, r, c - 1) - v2) * ss;
+            float dyy = (DOGV(im, P, r + 1, c) + DOGV(im, P, r - 1, c) - v2) * ss;
+            float dss = (DOGV(nx, P, r, c) + DOGV(pv, P, r, c) - v2) * ss;
+            float dxy = (DOGV(im, P, r + 1, c + 1) - DOGV(im, P, r + 1, c - 1) - DOGV(im, P, r - 1, c + 1) + DOGV(im, P, r - 1, c - 1)) * cs;
+            float dxs = (DOGV(nx, P, r, c + 1) - DOGV(nx, P, r, c - 1) - DOGV(pv, P, r, c + 1) + DOGV(pv, P, r, c - 1)) * cs;
+            float dys = (DOGV(nx, P, r + 1, c) - DOGV(nx, P, r - 1, c) - DOGV(pv, P, r + 1, c) + DOGV(pv, P, r - 1, c)) * cs;
             float H[9] = {dxx, dxy, dxs, dxy, dyy, dys, dxs, dys, dss};
             float X[3];
             solve3_dev(H, dD, X);
@@ -860,19 +854,20 @@ __global__ __launch_bounds__(64) void k_refine_orient(const Pyramid* __restrict_
         if (it >= VO_SIFT_MAX_INTERP) ok = false;
         float xo = 0, yo = 0, scl = 0, resp = 0;
         if (ok) {
-            const float* im = arena + g.d_off[layer] + img * g.plane;
-            const float* pv = arena + g.d_off[layer - 1] + img * g.plane;
-            const float* nx = arena + g.d_off[layer + 1] + img * g.plane;
-            float dD[3] = {(DAT(im, P, r, c + 1) - DAT(im, P, r, c - 1)) * ds,
-                           (DAT(im, P, r + 1, c) - DAT(im, P, r - 1, c)) * ds,
-                           (DAT(nx, P, r, c) - DAT(pv, P, r, c)) * ds};
+            const float* gb = arena + img * g.plane;
+            const float* im = gb + g.g_off[layer];          // DoG level l = G_{l+1} - G_l (VO_DOG)
+            const float* pv = gb + g.g_off[layer - 1];
+            const float* nx = gb + g.g_off[layer + 1];
+            float dD[3] = {(DOGV(im, P, r, c + 1) - DOGV(im, P, r, c - 1)) * ds,
+                           (DOGV(im, P, r + 1, c) - DOGV(im, P, r - 1, c)) * ds,
+                           (DOGV(nx, P, r, c) - DOGV(pv, P, r, c)) * ds};
             float tt = dD[0] * xc + dD[1] * xr + dD[2] * xi;
-            float contr = DAT(im, P, r, c) * img_scale + tt * 0.5f;
+            float contr = DOGV(im, P, r, c) * img_scale + tt * 0.5f;
             if (fabsf(contr) * (float)L < contrast_thr) ok = false;
-            float v2 = DAT(im, P, r, c) * 2.0f;
-            float dxx = (DAT(im, P, r, c + 1) + DAT(im, P, r, c - 1) - v2) * ss;
-            float dyy = (DAT(im, P, r + 1, c) + DAT(im, P, r - 1, c) - v2) * ss;
-            float dxy = (DAT(im, P, r + 1, c + 1) - DAT(im, P, r + 1, c - 1) - DAT(im, P, r - 1, c + 1) + DAT(im, P, r - 1, c - 1)) * cs;
+            float v2 = DOGV(im, P, r, c) * 2.0f;
+            float dxx = (DOGV(im, P, r, c + 1) + DOGV(im, P, r, c - 1) - v2) * ss;
+            float dyy = (DOGV(im, P, r + 1, c) + DOGV(im, P, r - 1, c) - v2) * ss;
+            float dxy = (DOGV(im, P, r + 1, c + 1) - DOGV(im, P, r + 1, c - 1) - DOGV(im, P, r - 1, c + 1) + DOGV(im, P, r - 1, c - 1)) * cs;
             float tr = dxx + dyy, det = dxx * dyy - dxy * dxy;
             if (det <= 0 || tr * tr * edge_thr >= (edge_thr + 1) * (edge_thr + 1) * det) ok = false;
             xo = (float)c + xc;
@@ -884,6 +879,7 @@ __global__ __launch_bounds__(64) void k_refine_orient(const Pyramid* __restrict_
             if (lane == 0) out->npk = 0;
             continue;
         }
+#undef DOGV
         // ---- orientation histogram ----
         const float* gim = arena + g.g_off[layer] + img * g.plane;
         const int radius = vo_round(VO_SIFT_ORI_RADIUS * scl);
@@ -1224,9 +1220,8 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
         if (R >= TH) {
             const int n_strips = (C + BS_W - 1) / BS_W, n_bands = (R + TH - 1) / TH;
             const int blocks = n_strips * n_bands * (int)grid.z;
-            const size_t lds = sizeof(float) * ((RAD + 1) * bs_rw(RAD) + 256);
-            VO_LAUNCH_NAMED("k_blur_fused", k_blur_stream<RAD>, dim3(blocks), dim3(64), lds, s, src, plane, pitch, R, C, g,
-                            d, K, n_strips, n_bands, TH);
+            VO_LAUNCH_NAMED("k_blur_fused", k_blur_stream<RAD>, dim3(blocks), dim3(64), 0, s, src, plane, pitch, R, C, g,
+                            K, n_strips, n_bands, TH);
             return;
         }
     }
@@ -1298,7 +1293,7 @@ void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_
         }
         for (int i = 1; i < L + 3; ++i) {
             Kern K = make_kern(py, i);
-            launch_blur<0>(gf, s, A + g.g_off[i - 1], g.plane, g.pitch, R, C, A + g.g_off[i], A + g.d_off[i - 1], K, src, 0, 0);
+            launch_blur<0>(gf, s, A + g.g_off[i - 1], g.plane, g.pitch, R, C, A + g.g_off[i], nullptr, K, src, 0, 0);
         }
     }
     const float thr = (float)floor(0.5 * p.contrast_threshold / L * 255.0);

@@ -47,16 +47,16 @@ extern Profiler* g_prof;
 // ---------------------------------------------------------------------------
 // Scale-space arena.  For each octave o and level i, the planes of all images
 // of a batch are contiguous: G(o,i,img) = arena + g_off[o][i] + img*plane[o].
-// Rows are padded to a multiple of 64 floats (256 B) so every row starts on a
-// cache-line boundary and a wave's 64 consecutive columns are one coalesced
-// 256-B access.
+// DoG planes are not stored: D(o,i) = G(o,i+1) - G(o,i) where it is consumed.
+// Rows are padded to a multiple of 256 floats (1 KiB): every row starts on a
+// cache-line boundary and spans a whole number of the level blur's 256-column
+// strips, so lanes past the last column store into padding instead of branching.
 // ---------------------------------------------------------------------------
 struct OctGeom {
     int rows, cols, pitch;
     int pad;
     size_t plane;                       // rows * pitch (floats)
     size_t g_off[VO_SIFT_MAX_LAYERS];   // L+3 Gaussian levels
-    size_t d_off[VO_SIFT_MAX_LAYERS];   // L+2 DoG levels
 };
 
 struct Pyramid {

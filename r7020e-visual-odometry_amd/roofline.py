@@ -3,10 +3,12 @@
 SURVEY §8(d) prices the SIFT scale space as a materialised fp32 pyramid in
 which every Gaussian and DoG level is written once and read once:
     B_img = W*H + 4 * (2*G + 2*D),  G = 6P, D = 5P,  P = sum of octave pixels.
-The per-kernel figures below split that model by the role each launch plays
-(bytes a kernel must move given its inputs and outputs, each touched once).
-They feed bench.py's `roofline.achieved` = bytes per launch / average launch
-duration of the dominant kernel.
+libvo never materialises the DoG planes (D = G_{i+1} - G_i is formed inside the
+extremum test and the refinement), so its kernels move fewer bytes than that
+model; `pyramid_bytes_per_image` keeps the SURVEY figure for comparison and
+`kernel_bytes` prices each launch by the bytes it must move given its own
+inputs and outputs, each touched once.  bench.py's `roofline.achieved` =
+bytes per launch / average launch duration of the dominant kernel.
 """
 from __future__ import annotations
 
@@ -49,7 +51,7 @@ def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3) -> dict:
         px = R * C * n_img
         if o:
             add("k_down", 8 * px, 1)                                      # 1 of 4 source px in, G0 out
-        add("k_blur_fused", 12 * px * lv, lv)                             # G_{i-1} in, G_i + D_{i-1} out
-    # extremum test reads the L+2 DoG levels of every octave once
-    add(f"k_ext_tile<{layers}>", sum(4 * (layers + 2) * r * c for r, c in dims) * n_img, 1)
+        add("k_blur_fused", 8 * px * lv, lv)                              # G_{i-1} in, G_i out
+    # extremum test reads the L+3 Gaussian levels of every octave once (DoG formed on chip)
+    add(f"k_ext_tile<{layers}>", sum(4 * (layers + 3) * r * c for r, c in dims) * n_img, 1)
     return out
