@@ -120,6 +120,51 @@ __device__ __forceinline__ float up_sample(const uint8_t* __restrict__ img, int 
     return 0.75f * ha + 0.25f * hb;
 }
 
+// Octave-0 source plane from the u8 image: the x2 upsample (UP) or a plain
+// u8 -> float conversion, 4 columns per thread, non-temporal 16-B stores.
+// Columns in [C, pitch) are padding and receive 0.
+template <bool UP>
+__global__ __launch_bounds__(256) void k_base_src(ImageSrc isrc, int in_rows, int in_cols, float* __restrict__ dst,
+                                                  size_t plane, int pitch, int R, int C, int n_img)
+{
+    // grid: x = 4-column groups (256 per block), y = row, z = image
+    const int y = blockIdx.y, img = blockIdx.z;
+    const int x = 4 * (blockIdx.x * 256 + threadIdx.x);
+    if (x >= pitch) return;
+    const uint8_t* base8 = ((img & 1) ? isrc.right : isrc.left) + (size_t)(img >> 1) * isrc.frame_stride;
+    float v[4];
+    const int g2 = x >> 1;                               // UP: source columns g2-1 .. g2+2 feed outputs x .. x+3
+    if (UP && g2 >= 1 && g2 + 5 < in_cols) {
+        // the 4 source bytes of rows ya, yb from two aligned 32-bit words each (unaligned ld)
+        const int ya = y >> 1, yb = (y & 1) ? (ya + 1 < in_rows ? ya + 1 : in_rows - 1) : (ya > 0 ? ya - 1 : 0);
+        float s[2][4];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint8_t* a = base8 + (size_t)(q ? yb : ya) * isrc.ld + g2 - 1;
+            const uintptr_t al = reinterpret_cast<uintptr_t>(a) & ~(uintptr_t)3;
+            const uint32_t w0 = *reinterpret_cast<const uint32_t*>(al), w1 = *reinterpret_cast<const uint32_t*>(al + 4);
+            const uint32_t b4 = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(reinterpret_cast<uintptr_t>(a) & 3));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) s[q][i] = (float)((b4 >> (8 * i)) & 0xff);
+        }
+        // s[.][0..3] = columns g2-1, g2, g2+1, g2+2 ; same expressions as up_sample
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int xa = 1 + (i >> 1), xb = (i & 1) ? xa + 1 : xa - 1;
+            const float ha = 0.75f * s[0][xa] + 0.25f * s[0][xb];
+            const float hb = 0.75f * s[1][xa] + 0.25f * s[1][xb];
+            v[i] = x + i < C ? 0.75f * ha + 0.25f * hb : 0.0f;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            v[i] = x + i < C ? (UP ? up_sample(base8, isrc.ld, in_rows, in_cols, y, x + i) : (float)base8[y * isrc.ld + x + i])
+                             : 0.0f;
+    }
+    typedef float f4_t __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(f4_t{v[0], v[1], v[2], v[3]}, reinterpret_cast<f4_t*>(dst + img * plane + (size_t)y * pitch + x));
+}
+
 // ---------------------------------------------------------------------------
 // Fused separable blur of one scale level + DoG (one launch per level).
 // A 64x64 output tile and its radius-r halo are staged once in LDS; the row
@@ -517,6 +562,88 @@ __global__ void k_down(const float* __restrict__ src, size_t splane, int spitch,
         int rem = (int)(t - (size_t)img * R * C);
         int y = rem / C, x = rem - y * C;
         dst[img * dplane + (size_t)y * dpitch + x] = src[img * splane + (size_t)(2 * y) * spitch + 2 * x];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Small octaves in one launch: one workgroup per image builds every level of
+// octaves o_first .. n_oct-1 in LDS (planes of <= VO_SMALL_PX pixels), so the
+// ~6 latency-bound launches per tiny octave (5 blurs + downsample) become one.
+// Octave o_first's base is the 2x decimation of G_L of octave o_first-1 (from
+// HBM); later bases are decimated from the LDS copy of G_L.  Every level is
+// written to its arena plane (the extremum test, refinement and descriptors
+// read them).  Per-output arithmetic = k_blur_fused (row pass, then column
+// pass, acc = k0*s0; acc = fmaf(kj, s[-j] + s[+j], acc)); reflect-101 indices
+// come from per-octave LDS tables.
+// ---------------------------------------------------------------------------
+#define VO_SMALL_PX 9216          // 3 planes + the next base fit in 160 KB of LDS
+#define VO_SMALL_T 1024
+
+__global__ __launch_bounds__(VO_SMALL_T) void k_small_pyr(const Pyramid* __restrict__ py, float* __restrict__ arena,
+                                                          int o_first, int rtab)
+{
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int img = blockIdx.x, tid = threadIdx.x;
+    const int L = py->L, NL = L + 3;
+    float* cur = sm;                                  // G_{i-1}
+    float* tmp = sm + VO_SMALL_PX;                    // row-pass output
+    float* nxt = sm + 2 * VO_SMALL_PX;                // G_i
+    float* base = sm + 3 * VO_SMALL_PX;               // next octave's G_0 (<= VO_SMALL_PX / 4)
+    int* ridx = reinterpret_cast<int*>(base + VO_SMALL_PX / 4);       // reflect-101 tables
+    int* cidx = ridx + rtab;                          // rtab >= rows + 2r of every octave here
+    for (int o = o_first; o < py->n_oct; ++o) {
+        const OctGeom& g = py->oct[o];
+        const int R = g.rows, C = g.cols, RC = R * C;
+        float* gplane = arena + img * g.plane;
+        // ---- G_0 ----
+        if (o == o_first) {
+            const OctGeom& pg = py->oct[o - 1];
+            const float* sp = arena + pg.g_off[L] + img * pg.plane;
+            for (int e = tid; e < RC; e += VO_SMALL_T) {
+                const int y = e / C, x = e - y * C;
+                cur[e] = sp[(size_t)(2 * y) * pg.pitch + 2 * x];
+            }
+        } else {
+            for (int e = tid; e < RC; e += VO_SMALL_T) cur[e] = base[e];
+        }
+        __syncthreads();
+        for (int e = tid; e < RC; e += VO_SMALL_T) {
+            const int y = e / C, x = e - y * C;
+            gplane[g.g_off[0] + (size_t)y * g.pitch + x] = cur[e];
+        }
+        // ---- levels 1 .. L+2 ----
+        for (int i = 1; i < NL; ++i) {
+            const int r = py->krad[i];
+            const float* kk = py->kern[i];
+            for (int t = tid; t < R + 2 * r; t += VO_SMALL_T) ridx[t] = vo_reflect101(t - r, R);
+            for (int t = tid; t < C + 2 * r; t += VO_SMALL_T) cidx[t] = vo_reflect101(t - r, C);
+            __syncthreads();
+            for (int e = tid; e < RC; e += VO_SMALL_T) {                 // row pass
+                const int y = e / C, x = e - y * C;
+                const float* row = cur + y * C;
+                float acc = kk[0] * row[x];
+                for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], row[cidx[x + r - j]] + row[cidx[x + r + j]], acc);
+                tmp[e] = acc;
+            }
+            __syncthreads();
+            for (int e = tid; e < RC; e += VO_SMALL_T) {                 // column pass
+                const int y = e / C, x = e - y * C;
+                float acc = kk[0] * tmp[e];
+                for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], tmp[ridx[y + r - j] * C + x] + tmp[ridx[y + r + j] * C + x], acc);
+                nxt[e] = acc;
+                gplane[g.g_off[i] + (size_t)y * g.pitch + x] = acc;
+            }
+            __syncthreads();
+            if (i == L && o + 1 < py->n_oct) {                           // next octave's base: decimated G_L
+                const int C2 = py->oct[o + 1].cols, R2 = py->oct[o + 1].rows;
+                for (int e = tid; e < R2 * C2; e += VO_SMALL_T) {
+                    const int y = e / C2, x = e - y * C2;
+                    base[e] = nxt[(2 * y) * C + 2 * x];
+                }
+            }
+            float* t2 = cur; cur = nxt; nxt = t2;
+        }
+        __syncthreads();
     }
 }
 
@@ -1210,18 +1337,24 @@ static Kern make_kern(const Pyramid& py, int level)
 
 template <int RAD, int MODE>
 static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t plane, int pitch, int R, int C, float* g,
-                          float* d, const Kern& K, const ImageSrc& isrc, int in_rows, int in_cols)
+                          float* d, const Kern& K, const ImageSrc& isrc, int in_rows, int in_cols, const char* name)
 {
     const size_t lds = sizeof(float) * ft_lds_floats(K.r);
     static const int use_pipe = getenv("VO_BLUR_PIPE") ? atoi(getenv("VO_BLUR_PIPE")) : 0;
     if constexpr (MODE == 0 && RAD > 0) if (!use_pipe) {
         static const int th_env = getenv("VO_BLUR_TH") ? atoi(getenv("VO_BLUR_TH")) : 48;
-        const int TH = std::max(BS_P, th_env / BS_P * BS_P);       // band height: a multiple of P
+        static const int wave_target = getenv("VO_BLUR_WAVES") ? atoi(getenv("VO_BLUR_WAVES")) : 2048;
+        // band height: a multiple of P, at most th_env, lowered on small octaves until
+        // the launch has ~wave_target waves (8 per CU) -- small planes are latency-bound
+        const int n_strips = (C + BS_W - 1) / BS_W;
+        const long rows_total = (long)R * n_strips * grid.z;
+        int TH = (int)std::min<long>(th_env, rows_total / wave_target);
+        TH = std::max(BS_P, TH / BS_P * BS_P);
         if (R >= TH) {
-            const int n_strips = (C + BS_W - 1) / BS_W, n_bands = (R + TH - 1) / TH;
+            const int n_bands = (R + TH - 1) / TH;
             const int blocks = n_strips * n_bands * (int)grid.z;
-            VO_LAUNCH_NAMED("k_blur_fused", k_blur_stream<RAD>, dim3(blocks), dim3(64), 0, s, src, plane, pitch, R, C, g,
-                            K, n_strips, n_bands, TH);
+            VO_LAUNCH_NAMED(name, k_blur_stream<RAD>, dim3(blocks), dim3(64), 0, s, src, plane, pitch, R, C, g, K,
+                            n_strips, n_bands, TH);
             return;
         }
     }
@@ -1239,7 +1372,7 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const int n_tiles = grid.x * grid.y * grid.z;
         const int blocks = std::min(n_tiles, per_cu * cus);
-        VO_LAUNCH_NAMED("k_blur_fused", k_blur_pipe<RAD>, dim3(blocks), dim3(256), lds, s, src, plane, pitch, R, C, g, d, K,
+        VO_LAUNCH_NAMED(name, k_blur_pipe<RAD>, dim3(blocks), dim3(256), lds, s, src, plane, pitch, R, C, g, d, K,
                         (int)grid.x, (int)grid.y, n_tiles);
         return;
     }
@@ -1256,15 +1389,16 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
 
 template <int MODE>
 static void launch_blur(dim3 grid, hipStream_t s, const float* src, size_t plane, int pitch, int R, int C, float* g,
-                        float* d, const Kern& K, const ImageSrc& isrc, int in_rows, int in_cols)
+                        float* d, const Kern& K, const ImageSrc& isrc, int in_rows, int in_cols,
+                        const char* name = MODE == 0 ? "k_blur_fused" : "k_blur_base")
 {
     switch (K.r) {
-    case 5: launch_blur_r<5, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols); break;
-    case 6: launch_blur_r<6, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols); break;
-    case 8: launch_blur_r<8, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols); break;
-    case 10: launch_blur_r<10, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols); break;
-    case 13: launch_blur_r<13, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols); break;
-    default: launch_blur_r<0, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols); break;
+    case 5: launch_blur_r<5, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
+    case 6: launch_blur_r<6, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
+    case 8: launch_blur_r<8, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
+    case 10: launch_blur_r<10, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
+    case 13: launch_blur_r<13, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
+    default: launch_blur_r<0, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
     }
 }
 
@@ -1273,15 +1407,47 @@ void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_
 {
     const int L = py.L;
     float* A = b.arena;
+    // first octave from which every remaining octave fits the one-launch LDS path
+    int o_small = py.n_oct, small_rtab = 0;
+    size_t small_lds = 0;
+    int maxr = 0;
+    for (int i = 1; i < L + 3; ++i) maxr = std::max(maxr, py.krad[i]);
+    for (int o = py.n_oct - 1; o >= 1; --o) {
+        int rt = 0, ct = 0;
+        bool fits = true;
+        for (int q = o; q < py.n_oct; ++q) {
+            fits = fits && py.oct[q].rows * py.oct[q].cols <= VO_SMALL_PX;
+            rt = std::max(rt, py.oct[q].rows + 2 * maxr);
+            ct = std::max(ct, py.oct[q].cols + 2 * maxr);
+        }
+        const size_t lds = sizeof(float) * (3 * VO_SMALL_PX + VO_SMALL_PX / 4) + sizeof(int) * (rt + ct);
+        if (!fits || lds > 160 * 1024) break;
+        o_small = o; small_rtab = rt; small_lds = lds;
+    }
     for (int o = 0; o < py.n_oct; ++o) {
         const OctGeom& g = py.oct[o];
         const int R = g.rows, C = g.cols;
+        if (o == o_small) {
+            static bool attr = false;
+            if (!attr) {
+                hipFuncSetAttribute((const void*)k_small_pyr, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                attr = true;
+            }
+            VO_LAUNCH_NAMED("k_blur_small", k_small_pyr, dim3(n_img), dim3(VO_SMALL_T), small_lds, s, d_py, A, o,
+                            small_rtab);
+            break;
+        }
         dim3 gf((C + FT_W - 1) / FT_W, (R + FT_H - 1) / FT_H, n_img);
         if (o == 0) {
             Kern K0 = make_kern(py, 0);
             const int rows = p.upsample ? R / 2 : R, cols = p.upsample ? C / 2 : C;
-            if (p.upsample) launch_blur<1>(gf, s, nullptr, g.plane, g.pitch, R, C, A + g.g_off[0], nullptr, K0, src, rows, cols);
-            else launch_blur<2>(gf, s, nullptr, g.plane, g.pitch, R, C, A + g.g_off[0], nullptr, K0, src, rows, cols);
+            // u8 (x2 upsampled) -> float source plane in the scratch buffer, then the level-0 blur
+            const dim3 qg((g.pitch / 4 + 255) / 256, R, n_img);
+            if (p.upsample)
+                VO_LAUNCH(k_base_src<true>, qg, dim3(256), 0, s, src, rows, cols, b.tmp, g.plane, g.pitch, R, C, n_img);
+            else
+                VO_LAUNCH(k_base_src<false>, qg, dim3(256), 0, s, src, rows, cols, b.tmp, g.plane, g.pitch, R, C, n_img);
+            launch_blur<0>(gf, s, b.tmp, g.plane, g.pitch, R, C, A + g.g_off[0], nullptr, K0, src, 0, 0, "k_blur_base");
         } else {
             const OctGeom& pg = py.oct[o - 1];
             size_t n = (size_t)n_img * R * C;

@@ -14,6 +14,8 @@ from __future__ import annotations
 
 import math
 
+SMALL_PX = 9216   # csrc/sift.hip VO_SMALL_PX
+
 
 def octave_dims(rows: int, cols: int, upsample: bool = True) -> list[tuple[int, int]]:
     R, C = (rows * 2, cols * 2) if upsample else (rows, cols)
@@ -46,9 +48,15 @@ def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3) -> dict:
         out[name] = (b + nbytes, l + launches)
 
     R0, C0 = dims[0]
-    add("k_blur_base", n_img * (rows * cols + 4 * R0 * C0), 1)           # u8 in (x2 upsample fused), G0 out
+    add("k_base_src<true>", n_img * (rows * cols + 4 * R0 * C0), 1)      # u8 in, x2-upsampled float plane out
+    add("k_blur_base", n_img * 8 * R0 * C0, 1)                            # source plane in, G0 out
+    # octaves from o_small on are built by one k_blur_small launch in LDS (planes <= SMALL_PX)
+    o_small = next((o for o in range(1, len(dims)) if all(r * c <= SMALL_PX for r, c in dims[o:])), len(dims))
     for o, (R, C) in enumerate(dims):
         px = R * C * n_img
+        if o >= o_small:
+            add("k_blur_small", 4 * px * (1 + lv), 1 if o == o_small else 0)  # decimated base in, G_0..G_{L+2} out
+            continue
         if o:
             add("k_down", 8 * px, 1)                                      # 1 of 4 source px in, G0 out
         add("k_blur_fused", 8 * px * lv, lv)                              # G_{i-1} in, G_i out
