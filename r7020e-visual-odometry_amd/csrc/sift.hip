@@ -56,25 +56,22 @@ void build_pyramid_geometry(Pyramid& py, int rows, int cols, int n_img, const vo
     vo_level_sigmas(L, p.sigma, sig);
     py.krad[0] = vo_gauss_kernel(vo_base_sigma(p.sigma, p.upsample), py.kern[0], VO_SIFT_MAX_RADIUS + 1);
     for (int i = 1; i < L + 3; ++i) py.krad[i] = vo_gauss_kernel(sig[i], py.kern[i], VO_SIFT_MAX_RADIUS + 1);
-    int w = 0, b = 0;
+    int w = 0, b = 0, t = 0;
     for (int o = 0; o < py.n_oct; ++o) {
         int ir = py.oct[o].rows - 2 * VO_SIFT_BORDER, ic = py.oct[o].cols - 2 * VO_SIFT_BORDER;
         if (ir < 0) ir = 0;
         if (ic < 0) ic = 0;
-        py.wrow[o] = (ic + 63) / 64;
+        // words of 64 absolute columns covering the interior [BORDER, cols - BORDER)
+        py.wrow[o] = ic > 0 ? (py.oct[o].cols - VO_SIFT_BORDER - 1) / 64 + 1 : 0;
         for (int l = 0; l < L; ++l) { py.wbase[b++] = w; w += ir * py.wrow[o]; }
+        py.ebase[o] = t;
+        py.estrips[o] = ic > 0 ? (py.wrow[o] + 1) / 2 : 0;
+        t += py.estrips[o] * ((ir + VO_EXT_BAND - 1) / VO_EXT_BAND);
     }
     py.wbase[b] = w;
     py.n_words = w;
-    int t = 0;
-    for (int o = 0; o < py.n_oct; ++o) {
-        int ir = py.oct[o].rows - 2 * VO_SIFT_BORDER;
-        if (ir < 0) ir = 0;
-        py.tbase[o] = t;
-        t += (ir + VO_EXT_TILE_ROWS - 1) / VO_EXT_TILE_ROWS * py.wrow[o];
-    }
-    py.tbase[py.n_oct] = t;
-    py.n_tiles = t;
+    py.ebase[py.n_oct] = t;
+    py.n_units = t;
     py.n_seg = (w + VO_SEG_WORDS - 1) / VO_SEG_WORDS;
 }
 
@@ -665,114 +662,145 @@ __device__ __forceinline__ void decode_word(const Pyramid* __restrict__ py, int 
 }
 
 // ---------------------------------------------------------------------------
-// 26-neighbour extremum test.  One block per tile of 64 interior columns x 16
-// interior rows of one octave; the tile (+1 halo) of all L+2 DoG levels is
-// staged in LDS once and serves all L layers (DoG read once, not 3x).  Wave w
-// owns tile rows 4w..4w+3; each lane keeps its 6x3 window of every level in
-// registers and tests 4 rows x L layers; one ballot per (row, layer) is the
-// 64-bit mask word of that row in (octave, layer, row, word) order.
+// 26-neighbour extremum test, streaming.  One wave per (image, octave, strip
+// of 128 columns, band of VO_EXT_BAND interior rows); lane l owns columns
+// xs+2l, xs+2l+1.  The wave walks the band's rows (+1 above and below): per
+// row it loads the L+3 Gaussian levels (8-B loads + one halo column each
+// side), forms D_l = G_{l+1} - G_l (never stored), reduces each level to its
+// horizontal 3-max/3-min (neighbours by lane shuffle), and keeps the last 3
+// rows of those in a register window (rows unrolled by 3, static slots).
+// Row t-1 is then tested: val >= max of its 3x3x3 block (val included)
+// <=> val >= all 26 neighbours.  Two ballots per (row, layer) are interleaved
+// into the two 64-column mask words of the strip.  Input rows are prefetched
+// 3 rows ahead.
 // ---------------------------------------------------------------------------
-#define ET_W 64
-#define ET_LW 68            // LDS row length (66 used)
-#define ET_LR (VO_EXT_TILE_ROWS + 2)
+__device__ __forceinline__ uint64_t vo_spread32(uint64_t x)     // bit i -> bit 2i
+{
+    x &= 0xffffffffull;
+    x = (x | (x << 16)) & 0x0000ffff0000ffffull;
+    x = (x | (x << 8)) & 0x00ff00ff00ff00ffull;
+    x = (x | (x << 4)) & 0x0f0f0f0f0f0f0f0full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
 
 template <int L>
-__global__ __launch_bounds__(256) void k_ext_tile(const Pyramid* __restrict__ py, const float* __restrict__ arena,
-                                                  unsigned long long* __restrict__ mask, float thr, int n_img)
+__global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ py, const float* __restrict__ arena,
+                                                   unsigned long long* __restrict__ mask, float thr, int n_img)
 {
-    __shared__ float lds[(L + 2) * ET_LR * ET_LW];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int nt = py->n_tiles, total = nt * n_img;
-    // persistent: block walks tiles T, T+grid, ...
-    auto locate = [&](int T, int& img, int& o, int& k, int& r0, int& c0) {
-        img = T / nt;
-        const int t = T - img * nt;
-        o = 0;
-        while (o + 1 < py->n_oct && py->tbase[o + 1] <= t) ++o;
-        const int wr = py->wrow[o], rel = t - py->tbase[o];
-        const int rb = rel / wr;
-        k = rel - rb * wr;
-        r0 = VO_SIFT_BORDER + rb * VO_EXT_TILE_ROWS;
-        c0 = VO_SIFT_BORDER + k * ET_W;
-    };
-    for (int T = blockIdx.x; T < total; T += gridDim.x) {
-        {
-            int img, o, k, r0, c0;
-            locate(T, img, o, k, r0, c0);
-            const OctGeom& g = py->oct[o];
-            // all loads issued back to back (level loop uniform -> scalar plane bases), then LDS writes
-            constexpr int PE = ET_LR * (ET_W + 2), PQ = (PE + 255) / 256;
-            int off[PQ];
+    constexpr int NG = L + 3, ND = L + 2, W = 3;      // Gaussian levels, DoG levels, row window
+    const int lane = threadIdx.x;
+    const int u_all = xcd_remap(blockIdx.x, gridDim.x);
+    const int nu = py->n_units;
+    const int img = u_all / nu;
+    int u = u_all - img * nu;
+    int o = 0;
+    while (o + 1 < py->n_oct && py->ebase[o + 1] <= u) ++o;
+    o = __builtin_amdgcn_readfirstlane(o);
+    u -= py->ebase[o];
+    const OctGeom& g = py->oct[o];
+    const int rows = g.rows, cols = g.cols, pitch = g.pitch;
+    const int ns = py->estrips[o];
+    const int strip = u % ns, band = u / ns;
+    const int ir = rows - 2 * VO_SIFT_BORDER;
+    const int r0 = VO_SIFT_BORDER + band * VO_EXT_BAND;                 // first tested row
+    const int nrow = min(VO_EXT_BAND, ir - band * VO_EXT_BAND);          // tested rows in this band
+    const int xs = strip * 128, xc = xs + 2 * lane;
+    // halo columns: lane 0 -> xs-1, lane 1 -> xs+128 (others reload lane 0's)
+    const int hx = lane == 1 ? xs + 128 : max(xs - 1, 0);
+    const float* base = arena + img * g.plane;
+    size_t goff[NG];
 #pragma unroll
-            for (int q = 0; q < PQ; ++q) {
-                const int e = tid + 256 * q;
-                const int rr = e / (ET_W + 2), cc = e - rr * (ET_W + 2);
-                off[q] = min(r0 - 1 + rr, g.rows - 1) * g.pitch + min(c0 - 1 + cc, g.cols - 1);
-            }
-            float tv[L + 3][PQ];                          // Gaussian levels 0 .. L+2
+    for (int lv = 0; lv < NG; ++lv) goff[lv] = g.g_off[lv];
+    const int wr = py->wrow[o];
+    unsigned long long* mrow = mask + (size_t)img * py->n_words;
+    const bool in0 = xc >= VO_SIFT_BORDER && xc < cols - VO_SIFT_BORDER;
+    const bool in1 = xc + 1 >= VO_SIFT_BORDER && xc + 1 < cols - VO_SIFT_BORDER;
+
+    typedef float f2_t __attribute__((ext_vector_type(2)));
+    f2_t pm[W][NG];                                  // prefetched main columns, per window slot
+    float ph[W][NG];                                 // prefetched halo column
+    f2_t hmx[W][ND], hmn[W][ND];                     // horizontal 3-max / 3-min per row slot
+    f2_t dc[W][L];                                   // D of layers 1..L per row slot (centres)
+
+#define VO_ET_LOAD(T, SL)                                                                          \
+    do {                                                                                           \
+        const int y_ = min(r0 - 1 + (T), rows - 1);                                                \
+        const float* rp_ = base + (size_t)y_ * pitch;                                              \
+        _Pragma("unroll") for (int lv = 0; lv < NG; ++lv) {                                        \
+            pm[SL][lv] = *reinterpret_cast<const f2_t*>(rp_ + goff[lv] + xc);                      \
+            ph[SL][lv] = rp_[goff[lv] + hx];                                                       \
+        }                                                                                          \
+    } while (0)
+
+    // one row step: D, horizontal reductions into slot SL; if TEST, test row in slot (SL+2)%3
+    auto step = [&](int t, auto sl_c, auto test_c) {
+        constexpr int SL = decltype(sl_c)::value;
+        f2_t d[ND];
+        float hd[ND];
 #pragma unroll
-            for (int lv = 0; lv < L + 3; ++lv) {
-                const float* pl = arena + g.g_off[lv] + img * g.plane;
-#pragma unroll
-                for (int q = 0; q < PQ; ++q)
-                    if (tid + 256 * q < PE) tv[lv][q] = pl[off[q]];
-            }
-#pragma unroll
-            for (int lv = 0; lv < L + 2; ++lv)            // D_lv = G_{lv+1} - G_lv
-#pragma unroll
-                for (int q = 0; q < PQ; ++q) {
-                    const int e = tid + 256 * q;
-                    if (e < PE) {
-                        const int rr = e / (ET_W + 2), cc = e - rr * (ET_W + 2);
-                        lds[(lv * ET_LR + rr) * ET_LW + cc] = tv[lv + 1][q] - tv[lv][q];
-                    }
-                }
+        for (int lv = 0; lv < ND; ++lv) {
+            d[lv] = pm[SL][lv + 1] - pm[SL][lv];
+            hd[lv] = ph[SL][lv + 1] - ph[SL][lv];
         }
-        __syncthreads();
-        int img, o, k, r0, c0;
-        locate(T, img, o, k, r0, c0);
-        const OctGeom& g = py->oct[o];
-        const int wr = py->wrow[o];
-        const int c = c0 + lane;
-        const bool cval = c < g.cols - VO_SIFT_BORDER;
-        // 3x3 max/min of every DoG level at this lane's column for the wave's 4 rows.
-        // val >= all 26 neighbours  <=>  val >= max of the 3x3x3 block (val included),
-        // and the per-level 3x3 extrema are shared by the adjacent layers.
-        float mx3[L + 2][4], mn3[L + 2][4], ctr[L + 2][4];
+        VO_ET_LOAD(t + W, SL);                        // refill the slot with row t+3
 #pragma unroll
-        for (int lv = 0; lv < L + 2; ++lv) {
-            float hmx[6], hmn[6];
-#pragma unroll
-            for (int a = 0; a < 6; ++a) {
-                const float* row = lds + (lv * ET_LR + 4 * w + a) * ET_LW + lane;
-                const float x0 = row[0], x1 = row[1], x2 = row[2];
-                hmx[a] = fmaxf(fmaxf(x0, x1), x2);
-                hmn[a] = fminf(fminf(x0, x1), x2);
-                if (a >= 1 && a <= 4) ctr[lv][a - 1] = x1;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                mx3[lv][q] = fmaxf(fmaxf(hmx[q], hmx[q + 1]), hmx[q + 2]);
-                mn3[lv][q] = fminf(fminf(hmn[q], hmn[q + 1]), hmn[q + 2]);
-            }
+        for (int lv = 0; lv < ND; ++lv) {
+            float left = __shfl_up(d[lv].y, 1);
+            float right = __shfl_down(d[lv].x, 1);
+            const float hr = __shfl(hd[lv], 1);
+            if (lane == 0) left = hd[lv];
+            if (lane == 63) right = hr;
+            const float m01 = fmaxf(d[lv].x, d[lv].y), n01 = fminf(d[lv].x, d[lv].y);
+            hmx[SL][lv] = f2_t{fmaxf(left, m01), fmaxf(m01, right)};
+            hmn[SL][lv] = f2_t{fminf(left, n01), fminf(n01, right)};
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int r = r0 + 4 * w + q;
-            const bool rval = r < g.rows - VO_SIFT_BORDER;
+        for (int l = 0; l < L; ++l) dc[SL][l] = d[l + 1];
+        if constexpr (decltype(test_c)::value) {
+            constexpr int A = (SL + 1) % W, M = (SL + 2) % W;   // rows t-2, t-1 (tested)
+            const int r = r0 + t - 2;
+            f2_t mx3[ND], mn3[ND];
+#pragma unroll
+            for (int lv = 0; lv < ND; ++lv) {
+                mx3[lv] = f2_t{fmaxf(fmaxf(hmx[A][lv].x, hmx[M][lv].x), hmx[SL][lv].x),
+                               fmaxf(fmaxf(hmx[A][lv].y, hmx[M][lv].y), hmx[SL][lv].y)};
+                mn3[lv] = f2_t{fminf(fminf(hmn[A][lv].x, hmn[M][lv].x), hmn[SL][lv].x),
+                               fminf(fminf(hmn[A][lv].y, hmn[M][lv].y), hmn[SL][lv].y)};
+            }
 #pragma unroll
             for (int layer = 1; layer <= L; ++layer) {
-                const float val = ctr[layer][q];
-                const float bmx = fmaxf(fmaxf(mx3[layer - 1][q], mx3[layer][q]), mx3[layer + 1][q]);
-                const float bmn = fminf(fminf(mn3[layer - 1][q], mn3[layer][q]), mn3[layer + 1][q]);
-                const bool ext = fabsf(val) > thr && ((val > 0 && val >= bmx) || (!(val > 0) && val <= bmn));
-                const unsigned long long bal = __ballot(ext && cval);
-                if (lane == 0 && rval)
-                    mask[(size_t)img * py->n_words + py->wbase[o * L + layer - 1] + (size_t)(r - VO_SIFT_BORDER) * wr + k] = bal;
+                bool e[2];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const float val = c ? dc[M][layer - 1].y : dc[M][layer - 1].x;
+                    const float bmx = fmaxf(fmaxf(c ? mx3[layer - 1].y : mx3[layer - 1].x, c ? mx3[layer].y : mx3[layer].x),
+                                            c ? mx3[layer + 1].y : mx3[layer + 1].x);
+                    const float bmn = fminf(fminf(c ? mn3[layer - 1].y : mn3[layer - 1].x, c ? mn3[layer].y : mn3[layer].x),
+                                            c ? mn3[layer + 1].y : mn3[layer + 1].x);
+                    e[c] = fabsf(val) > thr && ((val > 0 && val >= bmx) || (!(val > 0) && val <= bmn));
+                }
+                const uint64_t b0 = __ballot(e[0] && in0), b1 = __ballot(e[1] && in1);
+                const uint64_t w0 = vo_spread32(b0) | (vo_spread32(b1) << 1);
+                const uint64_t w1 = vo_spread32(b0 >> 32) | (vo_spread32(b1 >> 32) << 1);
+                const int k = 2 * strip + lane;
+                if (lane < 2 && k < wr && t - 2 < nrow)
+                    mrow[py->wbase[o * L + layer - 1] + (size_t)(r - VO_SIFT_BORDER) * wr + k] = lane ? w1 : w0;
             }
         }
-        __syncthreads();
+    };
+
+    vo_static_for<W>([&](auto c) { VO_ET_LOAD(decltype(c)::value, decltype(c)::value); });
+    step(0, std::integral_constant<int, 0>{}, std::false_type{});
+    step(1, std::integral_constant<int, 1>{}, std::false_type{});
+#pragma unroll 1
+    for (int t0 = 2; t0 < nrow + 2; t0 += W) {
+        step(t0, std::integral_constant<int, 2>{}, std::true_type{});
+        step(t0 + 1, std::integral_constant<int, 0>{}, std::true_type{});
+        step(t0 + 2, std::integral_constant<int, 1>{}, std::true_type{});
     }
+#undef VO_ET_LOAD
 }
 
 // Block-wide exclusive scan of one value per thread (1024 threads).
@@ -879,7 +907,7 @@ __global__ __launch_bounds__(256) void k_seg_emit(const Pyramid* __restrict__ py
         while (mm) {
             const int bit = __ffsll((long long)mm) - 1;
             mm &= mm - 1;
-            if (idx < (uint32_t)cand_cap) cand[(size_t)img * cand_cap + idx] = pack_cand(o, layer, r, VO_SIFT_BORDER + 64 * k + bit);
+            if (idx < (uint32_t)cand_cap) cand[(size_t)img * cand_cap + idx] = pack_cand(o, layer, r, 64 * k + bit);
             idx++;
         }
     }
@@ -1463,17 +1491,14 @@ void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_
         }
     }
     const float thr = (float)floor(0.5 * p.contrast_threshold / L * 255.0);
-    if (py.n_tiles > 0) {
-        int dev = 0, cus = 256;
-        hipGetDevice(&dev);
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const dim3 gt(std::min(py.n_tiles * n_img, 8 * cus));
+    if (py.n_units > 0) {
+        const dim3 ge(py.n_units * n_img);
         switch (L) {
-        case 1: VO_LAUNCH(k_ext_tile<1>, gt, dim3(256), 0, s, d_py, A, b.mask, thr, n_img); break;
-        case 2: VO_LAUNCH(k_ext_tile<2>, gt, dim3(256), 0, s, d_py, A, b.mask, thr, n_img); break;
-        case 3: VO_LAUNCH(k_ext_tile<3>, gt, dim3(256), 0, s, d_py, A, b.mask, thr, n_img); break;
-        case 4: VO_LAUNCH(k_ext_tile<4>, gt, dim3(256), 0, s, d_py, A, b.mask, thr, n_img); break;
-        default: VO_LAUNCH(k_ext_tile<5>, gt, dim3(256), 0, s, d_py, A, b.mask, thr, n_img); break;
+        case 1: VO_LAUNCH(k_ext_stream<1>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
+        case 2: VO_LAUNCH(k_ext_stream<2>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
+        case 3: VO_LAUNCH(k_ext_stream<3>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
+        case 4: VO_LAUNCH(k_ext_stream<4>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
+        default: VO_LAUNCH(k_ext_stream<5>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
         }
     }
     const dim3 gs(py.n_seg > 0 ? py.n_seg : 1, n_img);

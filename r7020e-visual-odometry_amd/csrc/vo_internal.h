@@ -66,17 +66,19 @@ struct Pyramid {
     int krad[VO_SIFT_MAX_LAYERS];
     size_t total;                        // floats in the arena
     size_t tmp_plane;                    // floats per image of the horizontal-pass scratch
-    // extrema word layout: words of 64 interior columns per (octave, layer, row)
+    // extrema word layout: per (octave, layer, interior row) the words of 64
+    // absolute columns [64k, 64k+64); bits of border columns are 0
     int wbase[VO_SIFT_MAX_OCTAVES * 4 + 1];   // prefix over (o, layer-1) blocks; size n_oct*L+1
     int wrow[VO_SIFT_MAX_OCTAVES];            // words per row in octave o
     int n_words;                              // words per image
-    // extremum-test tiles (64 interior columns x 16 interior rows, all layers)
-    int tbase[VO_SIFT_MAX_OCTAVES + 1];       // prefix of tiles per octave
-    int n_tiles;                              // tiles per image
+    // extremum-test units: (strip of 128 columns, band of VO_EXT_BAND interior rows)
+    int ebase[VO_SIFT_MAX_OCTAVES + 1];       // prefix of units per octave
+    int estrips[VO_SIFT_MAX_OCTAVES];         // strips per row in octave o
+    int n_units;                              // units per image
     int n_seg;                                // 1024-word compaction segments per image
 };
 
-#define VO_EXT_TILE_ROWS 16
+#define VO_EXT_BAND 30            // interior rows per extremum-test wave (a multiple of 3)
 #define VO_SEG_WORDS 1024
 
 // Packed candidate: c | r << 12 | layer << 24 | o << 27  (c, r < 4096)
