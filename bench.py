@@ -30,6 +30,9 @@ import numpy as np  # noqa: E402
 
 ROWS, COLS = 375, 1242
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+# per-launch HBM bytes of each kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes on this
+# workload (tools/pmc_passes.sh + tools/pmc_traffic.py; FETCH_SIZE doubled on gfx950)
+TRAFFIC_FILE = ROOT / "profiles" / "r01_pmc_traffic.json"
 
 
 def parse():
@@ -38,7 +41,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=16, help="stereo frames per step")
-    ap.add_argument("--cpu-frames", type=int, default=3, help="frames in the CPU-oracle baseline sample")
+    ap.add_argument("--cpu-frames", type=int, default=10, help="frames in the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3)
     return ap.parse_args()
@@ -104,6 +107,11 @@ def main():
     avg_ms = dom_ms / dom_calls
     roof = {"kernel": dom_name, "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
             "avg_launch_us": avg_ms * 1e3}
+    if TRAFFIC_FILE.exists():
+        tr = json.loads(TRAFFIC_FILE.read_text())["kernels"].get(dom_name)
+        if tr:
+            roof["traffic"] = tr["hbm_bytes_per_launch"]
+            roof["traffic_source"] = f"{TRAFFIC_FILE.relative_to(ROOT)} (PMC FETCH_SIZE x2 + WRITE_SIZE, per launch)"
     if dom_name in model:
         per_call_bytes, launches = model[dom_name]
         per_launch = per_call_bytes / launches

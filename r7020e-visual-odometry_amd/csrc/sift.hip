@@ -532,7 +532,7 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
 #undef VO_BS_LOAD
 }
 
-template <int RAD>
+template <int RAD, int TAG>   // TAG: 0 level blur, 1 octave-0 base (distinct symbol for the profilers)
 __global__ __launch_bounds__(64, RAD <= 6 ? 3 : 2) void k_blur_stream(const float* __restrict__ src, size_t plane, int pitch, int R, int C,
                                                     float* __restrict__ g_out, Kern K, int n_strips, int n_bands, int TH)
 {
@@ -1381,8 +1381,12 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
         if (R >= TH) {
             const int n_bands = (R + TH - 1) / TH;
             const int blocks = n_strips * n_bands * (int)grid.z;
-            VO_LAUNCH_NAMED(name, k_blur_stream<RAD>, dim3(blocks), dim3(64), 0, s, src, plane, pitch, R, C, g, K,
-                            n_strips, n_bands, TH);
+            if (name[7] == 'b')      // "k_blur_base"
+                VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, 1>), dim3(blocks), dim3(64), 0, s, src, plane, pitch, R, C, g, K,
+                                n_strips, n_bands, TH);
+            else
+                VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, 0>), dim3(blocks), dim3(64), 0, s, src, plane, pitch, R, C, g, K,
+                                n_strips, n_bands, TH);
             return;
         }
     }
