@@ -245,15 +245,18 @@ VO_HD uint32_t vo_rand_index(uint32_t r, uint32_t n) { return (uint32_t)(((uint6
 VO_HD int32_t vo_fx_quant(float v) { return (int32_t)rintf(v * VO_FX_SCALE); }
 VO_HD float vo_fx_to_float(int64_t s) { return (float)((double)s * (1.0 / 1048576.0)); }
 
-/* Descriptor histogram: unsigned 32-bit fixed point at 2^-10.  The gradient   */
-/* magnitude is pre-scaled by 2^10 (exact: a power of two), so each trilinear */
-/* share v >= 0 enters as rintf(v).  Overflow-free by construction: |dI| <=   */
-/* 255 so one share is < 361*2^10, and a spatial bin collects fewer than      */
-/* (2*hist_width+2)^2 <= 5.5e3 samples once the radius is capped at           */
-/* VO_SIFT_DESCR_RMAX (hist_width <= 36.3): < 2.1e9 < 2^32.                   */
+/* Orientation and descriptor histograms: unsigned 32-bit fixed point at     */
+/* 2^-10.  A weight v >= 0 is pre-scaled by 2^10 (exact: a power of two) and  */
+/* enters as rintf(v).  Overflow-free by construction, |dI| <= 255 so one     */
+/* weight is < 361*2^10:                                                      */
+/*  - descriptor: a spatial bin collects fewer than (2*hist_width+2)^2 <=     */
+/*    5.5e3 samples once the radius is capped at VO_SIFT_DESCR_RMAX           */
+/*    (hist_width <= 36.3): < 2.1e9 < 2^32;                                   */
+/*  - orientation: bins are summed in 64 bits (any window size).              */
 #define VO_DESC_FX_SCALE 1024.0f
 VO_HD uint32_t vo_desc_fx_quant(float v_scaled) { return (uint32_t)rintf(v_scaled); }
 VO_HD float vo_desc_fx_to_float(uint32_t s) { return (float)s * (1.0f / VO_DESC_FX_SCALE); }
+VO_HD float vo_hist_fx_to_float(uint64_t s) { return (float)s * (1.0f / VO_DESC_FX_SCALE); }
 
 /* ------------------------------------------------------------------------ */
 /* SIFT scale-space constants (spec, OpenCV-4.x conventions).  Computed on  */

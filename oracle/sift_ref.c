@@ -245,7 +245,7 @@ static int orientations(const float* img, int rows, int cols, int r, int c, floa
     int radius = vo_round(VO_SIFT_ORI_RADIUS * scl);
     float sigw = VO_SIFT_ORI_SIG * scl;
     float expf_scale = -1.0f / (2.0f * sigw * sigw);
-    int64_t hfx[VO_SIFT_ORI_BINS];
+    uint64_t hfx[VO_SIFT_ORI_BINS];
     memset(hfx, 0, sizeof(hfx));
     for (int i = -radius; i <= radius; ++i) {
         int y = r + i;
@@ -261,11 +261,11 @@ static int orientations(const float* img, int rows, int cols, int r, int c, floa
             int bin = vo_round((float)n / 360.0f * ori);
             if (bin >= n) bin -= n;
             if (bin < 0) bin += n;
-            hfx[bin] += vo_fx_quant(w * mag);
+            hfx[bin] += vo_desc_fx_quant((w * mag) * VO_DESC_FX_SCALE);
         }
     }
     float t[VO_SIFT_ORI_BINS], hist[VO_SIFT_ORI_BINS];
-    for (int k = 0; k < n; ++k) t[k] = vo_fx_to_float(hfx[k]);
+    for (int k = 0; k < n; ++k) t[k] = vo_hist_fx_to_float(hfx[k]);
     float maxval = 0.0f;
     for (int k = 0; k < n; ++k) {
         float m2 = t[(k + n - 2) % n], m1 = t[(k + n - 1) % n], p1 = t[(k + 1) % n], p2 = t[(k + 2) % n];

@@ -916,23 +916,44 @@ __global__ __launch_bounds__(256) void k_seg_emit(const Pyramid* __restrict__ py
 // ---------------------------------------------------------------------------
 // refinement + orientation: one wave (block of 64) per candidate
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool flat_item(const int* __restrict__ counts, int cap, int n_img, long t, int& img, int& k)
+// Flat item space over images: item t of image i is t - pre[i] for
+// pre[i] <= t < pre[i+1], pre[i+1] = pre[i] + min(counts[i], cap).  The prefix
+// is built once per block in LDS (all threads call flat_setup); flat_find is
+// then a binary search instead of a per-item walk over the images.
+#define VO_FLAT_MAX_IMG 130     // 2 * max_batch(64) + 2 image slots
+__device__ __forceinline__ long flat_setup(const int* __restrict__ counts, int cap, int n_img, int* pre)
 {
-    long acc = 0;
-    for (int i = 0; i < n_img; ++i) {
-        int c = counts[i];
-        if (c > cap) c = cap;
-        if (t < acc + c) { img = i; k = (int)(t - acc); return true; }
-        acc += c;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    __shared__ int carry;
+    if (tid == 0) { carry = 0; pre[0] = 0; }
+    __syncthreads();
+    for (int b0 = 0; b0 < n_img; b0 += 64) {          // the first wave scans 64 images per round
+        if (tid < 64) {
+            const int i = b0 + tid;
+            int c = i < n_img ? min(counts[i], cap) : 0;
+            int x = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(x, o); if (tid >= o) x += y; }
+            const int base = carry;
+            if (i < n_img) pre[i + 1] = base + x;
+            const int tot = __shfl(x, 63);
+            if (tid == 0) carry = base + tot;
+        }
+        __syncthreads();
     }
-    return false;
+    (void)nt;
+    return pre[n_img];
 }
 
-__device__ __forceinline__ long flat_total(const int* __restrict__ counts, int cap, int n_img)
+__device__ __forceinline__ void flat_find(const int* pre, int n_img, long t, int& img, int& k)
 {
-    long acc = 0;
-    for (int i = 0; i < n_img; ++i) { int c = counts[i]; acc += c > cap ? cap : c; }
-    return acc;
+    int lo = 0, hi = n_img - 1;                       // largest i with pre[i] <= t
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    img = lo;
+    k = (int)(t - pre[lo]);
 }
 
 #define DAT(p, P, y, x) ((p)[(size_t)(y) * (P) + (x)])
@@ -952,28 +973,30 @@ __device__ __forceinline__ void solve3_dev(const float H[9], const float b[3], f
     X[0] = (float)(x0 * inv); X[1] = (float)(x1 * inv); X[2] = (float)(x2 * inv);
 }
 
-__global__ __launch_bounds__(64) void k_refine_orient(const Pyramid* __restrict__ py, const float* __restrict__ arena,
-                                                      const uint32_t* __restrict__ cand, const int* __restrict__ n_cand,
-                                                      CandOut* __restrict__ cout, int cand_cap, int n_img,
-                                                      float contrast_thr, float edge_thr, float sigma)
+// Refinement (adjustLocalExtrema + contrast/edge tests): one LANE per candidate.
+// The interpolation loop is the same expression sequence as the oracle's; lanes
+// of a wave work on different candidates (divergent iteration counts are fine).
+// Writes the refined fields of CandOut with npk = -1 (accepted, orientation
+// pending) or 0 (rejected).
+__global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, const float* __restrict__ arena,
+                                                const uint32_t* __restrict__ cand, const int* __restrict__ n_cand,
+                                                CandOut* __restrict__ cout, int cand_cap, int n_img,
+                                                float contrast_thr, float edge_thr, float sigma)
 {
-    __shared__ unsigned long long hfx[VO_SIFT_ORI_BINS];
-    __shared__ float tf[VO_SIFT_ORI_BINS];
-    __shared__ float hs[VO_SIFT_ORI_BINS];
-    const int lane = threadIdx.x;
     const int L = py->L;
-    const long total = flat_total(n_cand, cand_cap, n_img);
-    for (long t = blockIdx.x; t < total; t += gridDim.x) {
+    __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
+    const long total = flat_setup(n_cand, cand_cap, n_img, fpre);
+    for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
         int img, kidx;
-        flat_item(n_cand, cand_cap, n_img, t, img, kidx);
-        const uint32_t pc = __builtin_amdgcn_readfirstlane(cand[(size_t)img * cand_cap + kidx]);   // wave-uniform -> scalar geometry loads
+        flat_find(fpre, n_img, t, img, kidx);
+        const uint32_t pc = cand[(size_t)img * cand_cap + kidx];
         const int c0 = pc & 4095, r0 = (pc >> 12) & 4095, layer0 = (pc >> 24) & 7, o = pc >> 27;
         const OctGeom& g = py->oct[o];
         const int rows = g.rows, cols = g.cols, P = g.pitch;
         const size_t lstride = g.g_off[1] - g.g_off[0];    // next Gaussian level of the same image
 #define DOGV(p, P, y, x) (DAT((p) + lstride, P, y, x) - DAT(p, P, y, x))
         CandOut* out = cout + (size_t)img * cand_cap + kidx;
-        // ---- adjustLocalExtrema (wave-uniform) ----
+        // ---- adjustLocalExtrema ----
         const float img_scale = 1.0f / 255.0f;
         const float ds = img_scale * 0.5f, ss = img_scale, cs = img_scale * 0.25f;
         int r = r0, c = c0, layer = layer0;
@@ -1030,35 +1053,86 @@ __global__ __launch_bounds__(64) void k_refine_orient(const Pyramid* __restrict_
             scl = sigma * vo_expf(((float)layer + xi) / (float)L * 0.693147181f);
             resp = fabsf(contr);
         }
-        if (!ok) {
-            if (lane == 0) out->npk = 0;
-            continue;
-        }
+        out->xo = xo; out->yo = yo; out->scl = scl; out->response = resp;
+        out->o = o; out->layer = layer; out->r = r; out->c = c;
+        out->npk = ok ? -1 : 0;
 #undef DOGV
+    }
+}
+
+// Orientation assignment: one wave per accepted candidate (npk == -1).  Each
+// lane accumulates its samples' fixed-point weights (vo_desc_fx_quant, 2^-10)
+// into a private LDS column hp[bin][lane] (no contention, conflict-free
+// banks); the 36 bins are then summed over the 64 lanes in 64 bits (integer
+// sums: identical to the oracle's sequential total).  Samples are processed 4
+// per lane per iteration with every gradient load issued first.  Smoothing,
+// peak test and interpolation as the oracle.  (A lane's u32 partial of one bin
+// holds < 11k samples' weights: windows up to ~7e5 samples.)
+__global__ __launch_bounds__(64) void k_orient(const Pyramid* __restrict__ py, const float* __restrict__ arena,
+                                               const int* __restrict__ n_cand, CandOut* __restrict__ cout,
+                                               int cand_cap, int n_img)
+{
+    __shared__ uint32_t hp[VO_SIFT_ORI_BINS * 64];
+    __shared__ float tf[VO_SIFT_ORI_BINS];
+    __shared__ float hs[VO_SIFT_ORI_BINS];
+    const int lane = threadIdx.x;
+    __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
+    const long total = flat_setup(n_cand, cand_cap, n_img, fpre);
+    for (long t = blockIdx.x; t < total; t += gridDim.x) {
+        int img, kidx;
+        flat_find(fpre, n_img, t, img, kidx);
+        CandOut* out = cout + (size_t)img * cand_cap + kidx;
+        if (__builtin_amdgcn_readfirstlane(out->npk) != -1) continue;
+        const int o = __builtin_amdgcn_readfirstlane(out->o), layer = __builtin_amdgcn_readfirstlane(out->layer);
+        const int r = __builtin_amdgcn_readfirstlane(out->r), c = __builtin_amdgcn_readfirstlane(out->c);
+        const float scl = out->scl;
+        const OctGeom& g = py->oct[o];
+        const int rows = g.rows, cols = g.cols, P = g.pitch;
         // ---- orientation histogram ----
         const float* gim = arena + g.g_off[layer] + img * g.plane;
         const int radius = vo_round(VO_SIFT_ORI_RADIUS * scl);
         const float sigw = VO_SIFT_ORI_SIG * scl;
         const float expf_scale = -1.0f / (2.0f * sigw * sigw);
-        if (lane < VO_SIFT_ORI_BINS) hfx[lane] = 0ull;
-        __syncthreads();
+#pragma unroll
+        for (int b2 = 0; b2 < VO_SIFT_ORI_BINS; ++b2) hp[b2 * 64 + lane] = 0u;
         const int side = 2 * radius + 1, nsamp = side * side;
-        for (int s = lane; s < nsamp; s += 64) {
-            const int i = s / side - radius, j = s - (s / side) * side - radius;
-            const int y = r + i, x = c + j;
-            if (y <= 0 || y >= rows - 1 || x <= 0 || x >= cols - 1) continue;
-            float dx = DAT(gim, P, y, x + 1) - DAT(gim, P, y, x - 1);
-            float dy = DAT(gim, P, y - 1, x) - DAT(gim, P, y + 1, x);
-            float w = vo_expf((float)(i * i + j * j) * expf_scale);
-            float mag = sqrtf(dx * dx + dy * dy);
-            float ori = vo_atan2_deg(dy, dx);
-            int bin = vo_round((float)VO_SIFT_ORI_BINS / 360.0f * ori);
-            if (bin >= VO_SIFT_ORI_BINS) bin -= VO_SIFT_ORI_BINS;
-            if (bin < 0) bin += VO_SIFT_ORI_BINS;
-            atomicAdd(&hfx[bin], (unsigned long long)(long long)vo_fx_quant(w * mag));
+        constexpr int U = 4;
+        for (int s0 = lane; s0 < nsamp; s0 += 64 * U) {
+            float gx[U], gy[U];
+            int ii[U], jj[U];
+            bool okk[U];
+#pragma unroll
+            for (int q = 0; q < U; ++q) {                 // indices, bounds, gradient loads
+                const int s = s0 + 64 * q;
+                const int i = s / side - radius, j = s - (s / side) * side - radius;
+                const int y = r + i, x = c + j;
+                ii[q] = i; jj[q] = j;
+                okk[q] = s < nsamp && y > 0 && y < rows - 1 && x > 0 && x < cols - 1;
+                gx[q] = 0.0f; gy[q] = 0.0f;
+                if (okk[q]) {
+                    gx[q] = DAT(gim, P, y, x + 1) - DAT(gim, P, y, x - 1);
+                    gy[q] = DAT(gim, P, y - 1, x) - DAT(gim, P, y + 1, x);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < U; ++q) {
+                if (!okk[q]) continue;
+                const float dx = gx[q], dy = gy[q];
+                float w = vo_expf((float)(ii[q] * ii[q] + jj[q] * jj[q]) * expf_scale);
+                float mag = sqrtf(dx * dx + dy * dy);
+                float ori = vo_atan2_deg(dy, dx);
+                int bin = vo_round((float)VO_SIFT_ORI_BINS / 360.0f * ori);
+                if (bin >= VO_SIFT_ORI_BINS) bin -= VO_SIFT_ORI_BINS;
+                if (bin < 0) bin += VO_SIFT_ORI_BINS;
+                hp[bin * 64 + lane] += vo_desc_fx_quant((w * mag) * VO_DESC_FX_SCALE);   // private column
+            }
         }
         __syncthreads();
-        if (lane < VO_SIFT_ORI_BINS) tf[lane] = vo_fx_to_float((int64_t)hfx[lane]);
+        if (lane < VO_SIFT_ORI_BINS) {
+            uint64_t acc = 0;                             // skewed walk: lanes hit distinct banks
+            for (int q = 0; q < 64; ++q) acc += hp[lane * 64 + ((q + lane) & 63)];
+            tf[lane] = vo_hist_fx_to_float(acc);
+        }
         __syncthreads();
         const int n = VO_SIFT_ORI_BINS;
         float hv = -INFINITY;
@@ -1090,12 +1164,8 @@ __global__ __launch_bounds__(64) void k_refine_orient(const Pyramid* __restrict_
             const int rank = __popcll(bal & ((1ull << lane) - 1ull));
             out->ang[rank] = ang;
         }
-        if (lane == 0) {
-            out->xo = xo; out->yo = yo; out->scl = scl; out->response = resp;
-            out->o = o; out->layer = layer; out->r = r; out->c = c;
-            out->npk = __popcll(bal);
-        }
         __syncthreads();
+        if (lane == 0) out->npk = __popcll(bal);
     }
 }
 
@@ -1123,10 +1193,11 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
                          vo_keypoint* __restrict__ kp, KpInt* __restrict__ kpi, int cand_cap, int kp_cap, int n_img,
                          int upsample)
 {
-    const long total = flat_total(n_cand, cand_cap, n_img);
+    __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
+    const long total = flat_setup(n_cand, cand_cap, n_img, fpre);
     for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
         int img, k;
-        flat_item(n_cand, cand_cap, n_img, t, img, k);
+        flat_find(fpre, n_img, t, img, k);
         const CandOut& co = cout[(size_t)img * cand_cap + k];
         const int npk = co.npk;
         if (!npk) continue;
@@ -1174,10 +1245,11 @@ __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, con
     __shared__ uint32_t hfx[DCOPIES * DHIST];
     __shared__ int rlo[2 * VO_SIFT_DESCR_RMAX + 2], rlen[2 * VO_SIFT_DESCR_RMAX + 2], rstart[2 * VO_SIFT_DESCR_RMAX + 3];
     const int lane = threadIdx.x;
-    const long total = flat_total(n_kp, kp_cap, n_img);
+    __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
+    const long total = flat_setup(n_kp, kp_cap, n_img, fpre);
     for (long t = blockIdx.x; t < total; t += gridDim.x) {
         int img, k;
-        flat_item(n_kp, kp_cap, n_img, t, img, k);
+        flat_find(fpre, n_img, t, img, k);
         KpInt q = kpi[(size_t)img * kp_cap + k];
         q.o = __builtin_amdgcn_readfirstlane(q.o);              // wave-uniform -> scalar geometry loads
         q.layer = __builtin_amdgcn_readfirstlane(q.layer);
@@ -1509,8 +1581,9 @@ void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_
     VO_LAUNCH(k_seg_count, gs, dim3(256), 0, s, b.mask, b.woff, py.n_words, py.n_seg);
     VO_LAUNCH(k_seg_scan, dim3(n_img), dim3(1024), 0, s, b.woff, b.n_cand, py.n_seg);
     VO_LAUNCH(k_seg_emit, gs, dim3(256), 0, s, d_py, b.mask, (const uint32_t*)b.woff, b.cand, b.cand_cap);
-    VO_LAUNCH(k_refine_orient, dim3(8192), dim3(64), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.cand_cap, n_img,
-                       p.contrast_threshold, p.edge_threshold, p.sigma);
+    VO_LAUNCH(k_refine, dim3(512), dim3(256), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.cand_cap, n_img,
+              p.contrast_threshold, p.edge_threshold, p.sigma);
+    VO_LAUNCH(k_orient, dim3(8192), dim3(64), 0, s, d_py, A, b.n_cand, b.cout, b.cand_cap, n_img);
     VO_LAUNCH(k_scan_cands, dim3(n_img), dim3(1024), 0, s, b.cout, b.n_cand, b.koff, b.n_kp, b.cand_cap);
     VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, b.n_cand, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
                        n_img, p.upsample);
