@@ -224,6 +224,13 @@ int vo_fetch_stereo_pairs(vo_ctx* ctx, int frame, uint32_t* pairs, int capacity,
  * timing over the last call (for bench.py's roofline; ms). */
 void* vo_stream(vo_ctx* ctx);
 int vo_set_profiling(vo_ctx* ctx, int enable);
+
+/* Batch calls (vo_sift_match_batch_dev, vo_step_batch*) split their frames over
+ * n_streams (1..4, default 2) HIP streams forked from / joined into vo_stream(),
+ * so latency-bound stages of one part overlap bandwidth-bound stages of
+ * another.  Results are identical for any n_streams.  While profiling is on,
+ * batches run as one part (clean per-kernel durations). */
+int vo_set_concurrency(vo_ctx* ctx, int n_streams);
 int vo_kernel_times(vo_ctx* ctx, const char** names, double* ms, int* calls, int capacity, int* n);
 
 #ifdef __cplusplus

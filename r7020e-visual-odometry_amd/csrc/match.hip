@@ -257,6 +257,15 @@ void match_free(MatchBuffers& b)
     b = MatchBuffers();
 }
 
+MatchBuffers match_view(const MatchBuffers& b, int k0)
+{
+    MatchBuffers v = b;
+    v.jobs = b.jobs ? b.jobs + k0 : nullptr;
+    v.partial = b.partial + (size_t)k0 * b.n_chunks * b.row_cap;
+    v.max_jobs = b.max_jobs - k0;
+    return v;
+}
+
 void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, const vo_match_params& p, hipStream_t s)
 {
     if (n_jobs <= 0) return;

@@ -47,10 +47,11 @@ void build_pyramid_geometry(Pyramid& py, int rows, int cols, int n_img, const vo
         g.rows = R; g.cols = C;
         g.pitch = (C + 255) / 256 * 256;    // whole 256-column blur strips: masked-off lanes store into padding
         g.plane = (size_t)g.rows * g.pitch;
-        for (int i = 0; i < L + 3; ++i) { g.g_off[i] = off; off += g.plane * n_img; }
+        for (int i = 0; i < L + 3; ++i) { g.g_off[i] = off; off += g.plane; }
         if (g.plane > tmp_plane) tmp_plane = g.plane;
     }
-    py.total = off;
+    py.istride = off;
+    py.total = off * n_img;
     py.tmp_plane = tmp_plane;
     double sig[VO_SIFT_MAX_LAYERS];
     vo_level_sigmas(L, p.sigma, sig);
@@ -73,6 +74,26 @@ void build_pyramid_geometry(Pyramid& py, int rows, int cols, int n_img, const vo
     py.ebase[py.n_oct] = t;
     py.n_units = t;
     py.n_seg = (w + VO_SEG_WORDS - 1) / VO_SEG_WORDS;
+}
+
+SiftBuffers sift_view(const SiftBuffers& b, const Pyramid& py, int img0, int n)
+{
+    SiftBuffers v = b;
+    v.arena = b.arena + (size_t)img0 * py.istride;
+    v.tmp = b.tmp + (size_t)img0 * py.tmp_plane;
+    v.mask = b.mask + (size_t)img0 * py.n_words;
+    v.woff = b.woff + (size_t)img0 * py.n_seg;
+    v.cand = b.cand + (size_t)img0 * b.cand_cap;
+    v.n_cand = b.n_cand + img0;
+    v.cout = b.cout + (size_t)img0 * b.cand_cap;
+    v.koff = b.koff + (size_t)img0 * b.cand_cap;
+    v.n_kp = b.n_kp + img0;
+    v.kp = b.kp + (size_t)img0 * b.kp_cap;
+    v.kpi = b.kpi + (size_t)img0 * b.kp_cap;
+    v.desc = b.desc + (size_t)img0 * b.kp_cap * VO_DESC_LEN;
+    v.meta = b.meta + (size_t)img0 * b.kp_cap;
+    v.n_img = n;
+    return v;
 }
 
 hipError_t sift_alloc(SiftBuffers& b, const Pyramid& py, int kp_cap, int cand_cap)
@@ -185,7 +206,7 @@ __host__ __device__ constexpr int ft_iw(int r) { return (FT_W + 2 * r + 3) & ~3;
 __host__ __device__ constexpr int ft_lds_floats(int r) { return (FT_H + 2 * r) * ft_iw(r) + (FT_H + 2 * r) * FT_HW; }
 
 template <int RAD, int MODE>
-__global__ __launch_bounds__(256) void k_blur_fused(const float* __restrict__ src, size_t plane, int pitch, int R, int C,
+__global__ __launch_bounds__(256) void k_blur_fused(const float* __restrict__ src, size_t plane, size_t dplane, int pitch, int R, int C,
                                                     float* __restrict__ g_out, float* __restrict__ d_out, Kern K,
                                                     ImageSrc isrc, int in_rows, int in_cols)
 {
@@ -273,7 +294,7 @@ __global__ __launch_bounds__(256) void k_blur_fused(const float* __restrict__ sr
             for (int i = 0; i < FT_V; ++i) {
                 const int y = y0 + y0l + i;
                 if (y < R) {
-                    const size_t o = img * plane + (size_t)y * pitch + x;
+                    const size_t o = img * dplane + (size_t)y * pitch + x;
                     g_out[o] = out[i];
                     if (MODE == 0 && d_out) d_out[o] = out[i] - in[(y0l + i + r) * IW + c + r];
                 }
@@ -291,7 +312,7 @@ __global__ __launch_bounds__(256) void k_blur_fused(const float* __restrict__ sr
 // HBM round trip behind a barrier.
 // ---------------------------------------------------------------------------
 template <int RAD>
-__global__ __launch_bounds__(256) void k_blur_pipe(const float* __restrict__ src, size_t plane, int pitch, int R, int C,
+__global__ __launch_bounds__(256) void k_blur_pipe(const float* __restrict__ src, size_t plane, size_t dplane, int pitch, int R, int C,
                                                    float* __restrict__ g_out, float* __restrict__ d_out, Kern K,
                                                    int tiles_x, int tiles_y, int n_tiles)
 {
@@ -368,7 +389,7 @@ __global__ __launch_bounds__(256) void k_blur_pipe(const float* __restrict__ src
                     for (int j = 1; j <= RAD; ++j) acc = fmaf(K.k[j], v[i + RAD - j] + v[i + RAD + j], acc);
                     const int y = y0 + y0l + i;
                     if (y < R) {
-                        const size_t o = img * plane + (size_t)y * pitch + x;
+                        const size_t o = img * dplane + (size_t)y * pitch + x;
                         g_out[o] = acc;
                         if (d_out) d_out[o] = acc - in[(y0l + i + RAD) * IW + c + RAD];
                     }
@@ -533,8 +554,9 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
 }
 
 template <int RAD, int TAG>   // TAG: 0 level blur, 1 octave-0 base (distinct symbol for the profilers)
-__global__ __launch_bounds__(64, RAD <= 6 ? 3 : 2) void k_blur_stream(const float* __restrict__ src, size_t plane, int pitch, int R, int C,
-                                                    float* __restrict__ g_out, Kern K, int n_strips, int n_bands, int TH)
+__global__ __launch_bounds__(64, RAD <= 6 ? 3 : 2) void k_blur_stream(const float* __restrict__ src, size_t splane, size_t dplane,
+                                                    int pitch, int R, int C, float* __restrict__ g_out, Kern K,
+                                                    int n_strips, int n_bands, int TH)
 {
     constexpr int R4 = bs_r4(RAD);
     __shared__ __attribute__((aligned(16))) float rb[bs_rw(RAD) + 256];   // staged row + per-lane dummy halo slots
@@ -542,11 +564,11 @@ __global__ __launch_bounds__(64, RAD <= 6 ? 3 : 2) void k_blur_stream(const floa
     const int strip = bid % n_strips, tb = bid / n_strips;
     const int band = tb % n_bands, img = tb / n_bands;
     const int x0 = strip * BS_W, y0 = min(band * TH, R - TH);
-    const size_t ob = img * plane;
+    const size_t os = img * splane, od = img * dplane;
     if (x0 - R4 < 0 || x0 + BS_W + R4 > C)
-        blur_stream_body<RAD, true>(src + ob, pitch, R, C, g_out + ob, K, x0, y0, TH, rb);
+        blur_stream_body<RAD, true>(src + os, pitch, R, C, g_out + od, K, x0, y0, TH, rb);
     else
-        blur_stream_body<RAD, false>(src + ob, pitch, R, C, g_out + ob, K, x0, y0, TH, rb);
+        blur_stream_body<RAD, false>(src + os, pitch, R, C, g_out + od, K, x0, y0, TH, rb);
 }
 
 // next octave base.  grid over outputs
@@ -591,11 +613,11 @@ __global__ __launch_bounds__(VO_SMALL_T) void k_small_pyr(const Pyramid* __restr
     for (int o = o_first; o < py->n_oct; ++o) {
         const OctGeom& g = py->oct[o];
         const int R = g.rows, C = g.cols, RC = R * C;
-        float* gplane = arena + img * g.plane;
+        float* gplane = arena + img * py->istride;
         // ---- G_0 ----
         if (o == o_first) {
             const OctGeom& pg = py->oct[o - 1];
-            const float* sp = arena + pg.g_off[L] + img * pg.plane;
+            const float* sp = arena + pg.g_off[L] + img * py->istride;
             for (int e = tid; e < RC; e += VO_SMALL_T) {
                 const int y = e / C, x = e - y * C;
                 cur[e] = sp[(size_t)(2 * y) * pg.pitch + 2 * x];
@@ -709,7 +731,7 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
     const int xs = strip * 128, xc = xs + 2 * lane;
     // halo columns: lane 0 -> xs-1, lane 1 -> xs+128 (others reload lane 0's)
     const int hx = lane == 1 ? xs + 128 : max(xs - 1, 0);
-    const float* base = arena + img * g.plane;
+    const float* base = arena + img * py->istride;
     size_t goff[NG];
 #pragma unroll
     for (int lv = 0; lv < NG; ++lv) goff[lv] = g.g_off[lv];
@@ -1004,7 +1026,7 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
         int it = 0;
         bool ok = true;
         for (; it < VO_SIFT_MAX_INTERP; ++it) {
-            const float* gb = arena + img * g.plane;
+            const float* gb = arena + img * py->istride;
             const float* im = gb + g.g_off[layer];          // DoG level l = G_{l+1} - G_l (VO_DOG)
             const float* pv = gb + g.g_off[layer - 1];
             const float* nx = gb + g.g_off[layer + 1];
@@ -1032,7 +1054,7 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
         if (it >= VO_SIFT_MAX_INTERP) ok = false;
         float xo = 0, yo = 0, scl = 0, resp = 0;
         if (ok) {
-            const float* gb = arena + img * g.plane;
+            const float* gb = arena + img * py->istride;
             const float* im = gb + g.g_off[layer];          // DoG level l = G_{l+1} - G_l (VO_DOG)
             const float* pv = gb + g.g_off[layer - 1];
             const float* nx = gb + g.g_off[layer + 1];
@@ -1089,7 +1111,7 @@ __global__ __launch_bounds__(64) void k_orient(const Pyramid* __restrict__ py, c
         const OctGeom& g = py->oct[o];
         const int rows = g.rows, cols = g.cols, P = g.pitch;
         // ---- orientation histogram ----
-        const float* gim = arena + g.g_off[layer] + img * g.plane;
+        const float* gim = arena + g.g_off[layer] + img * py->istride;
         const int radius = vo_round(VO_SIFT_ORI_RADIUS * scl);
         const float sigw = VO_SIFT_ORI_SIG * scl;
         const float expf_scale = -1.0f / (2.0f * sigw * sigw);
@@ -1255,7 +1277,7 @@ __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, con
         q.layer = __builtin_amdgcn_readfirstlane(q.layer);
         const OctGeom& g = py->oct[q.o];
         const int rows = g.rows, cols = g.cols, P = g.pitch;
-        const float* gim = arena + g.g_off[q.layer] + img * g.plane;
+        const float* gim = arena + g.g_off[q.layer] + img * py->istride;
         for (int b = lane; b < DCOPIES * DHIST; b += 64) hfx[b] = 0u;
         float ori = 360.0f - q.angle;
         if (fabsf(ori - 360.0f) < VO_FLT_EPSILON) ori = 0.0f;
@@ -1436,8 +1458,8 @@ static Kern make_kern(const Pyramid& py, int level)
 }
 
 template <int RAD, int MODE>
-static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t plane, int pitch, int R, int C, float* g,
-                          float* d, const Kern& K, const ImageSrc& isrc, int in_rows, int in_cols, const char* name)
+static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t plane, size_t dplane, int pitch, int R, int C,
+                          float* g, float* d, const Kern& K, const ImageSrc& isrc, int in_rows, int in_cols, const char* name)
 {
     const size_t lds = sizeof(float) * ft_lds_floats(K.r);
     static const int use_pipe = getenv("VO_BLUR_PIPE") ? atoi(getenv("VO_BLUR_PIPE")) : 0;
@@ -1454,11 +1476,11 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
             const int n_bands = (R + TH - 1) / TH;
             const int blocks = n_strips * n_bands * (int)grid.z;
             if (name[7] == 'b')      // "k_blur_base"
-                VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, 1>), dim3(blocks), dim3(64), 0, s, src, plane, pitch, R, C, g, K,
-                                n_strips, n_bands, TH);
+                VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, 1>), dim3(blocks), dim3(64), 0, s, src, plane, dplane, pitch, R,
+                                C, g, K, n_strips, n_bands, TH);
             else
-                VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, 0>), dim3(blocks), dim3(64), 0, s, src, plane, pitch, R, C, g, K,
-                                n_strips, n_bands, TH);
+                VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, 0>), dim3(blocks), dim3(64), 0, s, src, plane, dplane, pitch, R,
+                                C, g, K, n_strips, n_bands, TH);
             return;
         }
     }
@@ -1476,7 +1498,7 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const int n_tiles = grid.x * grid.y * grid.z;
         const int blocks = std::min(n_tiles, per_cu * cus);
-        VO_LAUNCH_NAMED(name, k_blur_pipe<RAD>, dim3(blocks), dim3(256), lds, s, src, plane, pitch, R, C, g, d, K,
+        VO_LAUNCH_NAMED(name, k_blur_pipe<RAD>, dim3(blocks), dim3(256), lds, s, src, plane, dplane, pitch, R, C, g, d, K,
                         (int)grid.x, (int)grid.y, n_tiles);
         return;
     }
@@ -1488,21 +1510,21 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
         }
     }
     VO_LAUNCH_NAMED(MODE == 0 ? "k_blur_fused" : "k_blur_base", (k_blur_fused<RAD, MODE>), grid, dim3(256), lds, s, src,
-                    plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols);
+                    plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols);
 }
 
 template <int MODE>
-static void launch_blur(dim3 grid, hipStream_t s, const float* src, size_t plane, int pitch, int R, int C, float* g,
+static void launch_blur(dim3 grid, hipStream_t s, const float* src, size_t plane, size_t dplane, int pitch, int R, int C, float* g,
                         float* d, const Kern& K, const ImageSrc& isrc, int in_rows, int in_cols,
                         const char* name = MODE == 0 ? "k_blur_fused" : "k_blur_base")
 {
     switch (K.r) {
-    case 5: launch_blur_r<5, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
-    case 6: launch_blur_r<6, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
-    case 8: launch_blur_r<8, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
-    case 10: launch_blur_r<10, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
-    case 13: launch_blur_r<13, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
-    default: launch_blur_r<0, MODE>(grid, s, src, plane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
+    case 5: launch_blur_r<5, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
+    case 6: launch_blur_r<6, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
+    case 8: launch_blur_r<8, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
+    case 10: launch_blur_r<10, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
+    case 13: launch_blur_r<13, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
+    default: launch_blur_r<0, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
     }
 }
 
@@ -1551,19 +1573,21 @@ void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_
                 VO_LAUNCH(k_base_src<true>, qg, dim3(256), 0, s, src, rows, cols, b.tmp, g.plane, g.pitch, R, C, n_img);
             else
                 VO_LAUNCH(k_base_src<false>, qg, dim3(256), 0, s, src, rows, cols, b.tmp, g.plane, g.pitch, R, C, n_img);
-            launch_blur<0>(gf, s, b.tmp, g.plane, g.pitch, R, C, A + g.g_off[0], nullptr, K0, src, 0, 0, "k_blur_base");
+            launch_blur<0>(gf, s, b.tmp, g.plane, py.istride, g.pitch, R, C, A + g.g_off[0], nullptr, K0, src, 0, 0,
+                           "k_blur_base");
         } else {
             const OctGeom& pg = py.oct[o - 1];
             size_t n = (size_t)n_img * R * C;
             int blocks = (int)((n + 255) / 256);
             if (blocks > 4096) blocks = 4096;
             if (blocks < 1) blocks = 1;
-            VO_LAUNCH(k_down, dim3(blocks), dim3(256), 0, s, A + pg.g_off[L], pg.plane, pg.pitch, A + g.g_off[0],
-                      g.plane, g.pitch, R, C, n_img);
+            VO_LAUNCH(k_down, dim3(blocks), dim3(256), 0, s, A + pg.g_off[L], py.istride, pg.pitch, A + g.g_off[0],
+                      py.istride, g.pitch, R, C, n_img);
         }
         for (int i = 1; i < L + 3; ++i) {
             Kern K = make_kern(py, i);
-            launch_blur<0>(gf, s, A + g.g_off[i - 1], g.plane, g.pitch, R, C, A + g.g_off[i], nullptr, K, src, 0, 0);
+            launch_blur<0>(gf, s, A + g.g_off[i - 1], py.istride, py.istride, g.pitch, R, C, A + g.g_off[i], nullptr, K, src,
+                           0, 0);
         }
     }
     const float thr = (float)floor(0.5 * p.contrast_threshold / L * 255.0);

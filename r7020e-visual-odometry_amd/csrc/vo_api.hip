@@ -62,6 +62,13 @@ struct vo_ctx {
     vo_calib calib;
     bool has_calib = false;
     hipStream_t stream = nullptr;
+    // sub-batch concurrency: a batch's frames are split over n_sub streams that
+    // fork from / join into `stream` (latency-bound SIFT stages of one part
+    // overlap bandwidth-bound stages of another)
+    static constexpr int MAX_SUB = 4;
+    int n_sub = 2;
+    hipStream_t sub[MAX_SUB] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[MAX_SUB] = {};
     Pyramid py;
     Pyramid* d_py = nullptr;
     SiftBuffers sb;                  // 2*max_batch + 2 image slots (last 2 = carried frame)
@@ -126,6 +133,17 @@ static int job_stereo(const vo_ctx*, int f) { return f; }
 static int job_track(const vo_ctx* c, int step, int f) { return c->max_batch + step * c->max_batch + f; }
 static int job_single(const vo_ctx* c) { return 5 * c->max_batch; }
 
+static void destroy_streams(vo_ctx* c)
+{
+    for (int k = 0; k < vo_ctx::MAX_SUB; ++k) {
+        if (c->sub[k]) hipStreamDestroy(c->sub[k]);
+        if (c->ev_join[k]) hipEventDestroy(c->ev_join[k]);
+        c->sub[k] = nullptr; c->ev_join[k] = nullptr;
+    }
+    if (c->ev_fork) hipEventDestroy(c->ev_fork);
+    c->ev_fork = nullptr;
+}
+
 static void destroy_buffers(vo_ctx* c)
 {
     sift_free(c->sb);
@@ -159,12 +177,18 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
     auto bail = [&](const char* what, hipError_t e) -> vo_ctx* {
         fail(nullptr, VO_ERR_HIP, "vo_create: %s: %s", what, hipGetErrorString(e));
         destroy_buffers(c);
+        destroy_streams(c);
         if (c->stream) hipStreamDestroy(c->stream);
         delete c;
         return nullptr;
     };
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bail("stream", e);
+    for (int k = 0; k < vo_ctx::MAX_SUB; ++k) {
+        if ((e = hipStreamCreateWithFlags(&c->sub[k], hipStreamNonBlocking)) != hipSuccess) return bail("stream", e);
+        if ((e = hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
+    }
+    if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("event", e);
     const int n_slots = 2 * max_batch + 2;
     const int kp_cap = c->sp.max_keypoints;
     build_pyramid_geometry(c->py, rows, cols, n_slots, c->sp);
@@ -219,8 +243,16 @@ void vo_destroy(vo_ctx* c)
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     destroy_buffers(c);
+    destroy_streams(c);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
+}
+
+int vo_set_concurrency(vo_ctx* c, int n_streams)
+{
+    if (!c || n_streams < 1 || n_streams > vo_ctx::MAX_SUB) return VO_ERR_ARG;
+    c->n_sub = n_streams;
+    return VO_OK;
 }
 
 int vo_set_calib(vo_ctx* c, const vo_calib* calib)
@@ -324,9 +356,29 @@ int vo_match(vo_ctx* c, const uint8_t* F1, int n1, const uint8_t* F2, int n2, ui
 // SIFT + stereo match on B frames already in device memory.
 static int enqueue_sift_stereo(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B)
 {
-    ImageSrc src{d_l, d_r, (size_t)c->rows * c->cols, c->cols, 0};
-    sift_enqueue(c->py, c->sb, src, 2 * B, c->sp, c->stream, c->d_py);
-    match_launch(c->mb, c->d_jobs + job_stereo(c, 0), B, c->mp, c->stream);
+    const size_t fs = (size_t)c->rows * c->cols;
+    // per-kernel profiling wants undisturbed launch durations: one part then
+    const int parts = c->prof.on ? 1 : std::min(c->n_sub, B);
+    if (parts <= 1) {
+        ImageSrc src{d_l, d_r, fs, c->cols, 0};
+        sift_enqueue(c->py, c->sb, src, 2 * B, c->sp, c->stream, c->d_py);
+        match_launch(c->mb, c->d_jobs + job_stereo(c, 0), B, c->mp, c->stream);
+        return VO_OK;
+    }
+    // fork: frames [f0, f1) of part p run SIFT + stereo matching on sub[p] over
+    // image-range views of the same buffers (image-major layouts), then join
+    HIPC(c, hipEventRecord(c->ev_fork, c->stream));
+    for (int p = 0; p < parts; ++p) {
+        const int f0 = B * p / parts, f1 = B * (p + 1) / parts, nf = f1 - f0;
+        hipStream_t s = c->sub[p];
+        HIPC(c, hipStreamWaitEvent(s, c->ev_fork, 0));
+        ImageSrc src{d_l + f0 * fs, d_r + f0 * fs, fs, c->cols, 0};
+        SiftBuffers v = sift_view(c->sb, c->py, 2 * f0, 2 * nf);
+        sift_enqueue(c->py, v, src, 2 * nf, c->sp, s, c->d_py);
+        match_launch(match_view(c->mb, job_stereo(c, f0)), c->d_jobs + job_stereo(c, f0), nf, c->mp, s);
+        HIPC(c, hipEventRecord(c->ev_join[p], s));
+        HIPC(c, hipStreamWaitEvent(c->stream, c->ev_join[p], 0));
+    }
     return VO_OK;
 }
 

@@ -45,8 +45,9 @@ extern Profiler* g_prof;
     VO_LAUNCH_NAMED(#kernel, kernel, grid, block, shmem, stream, __VA_ARGS__)
 
 // ---------------------------------------------------------------------------
-// Scale-space arena.  For each octave o and level i, the planes of all images
-// of a batch are contiguous: G(o,i,img) = arena + g_off[o][i] + img*plane[o].
+// Scale-space arena, image-major: the whole pyramid of one image is contiguous,
+// G(o,i,img) = arena + img*istride + g_off[o][i], so any contiguous range of
+// images is a pointer shift (sub-batches run concurrently on separate streams).
 // DoG planes are not stored: D(o,i) = G(o,i+1) - G(o,i) where it is consumed.
 // Rows are padded to a multiple of 256 floats (1 KiB): every row starts on a
 // cache-line boundary and spans a whole number of the level blur's 256-column
@@ -64,6 +65,7 @@ struct Pyramid {
     OctGeom oct[VO_SIFT_MAX_OCTAVES];
     float kern[VO_SIFT_MAX_LAYERS][VO_SIFT_MAX_RADIUS + 1];  // level blur kernels (level 0 = base)
     int krad[VO_SIFT_MAX_LAYERS];
+    size_t istride;                      // floats per image (all octaves and levels)
     size_t total;                        // floats in the arena
     size_t tmp_plane;                    // floats per image of the horizontal-pass scratch
     // extrema word layout: per (octave, layer, interior row) the words of 64
@@ -135,6 +137,8 @@ struct ImageSrc {
 };
 
 void build_pyramid_geometry(Pyramid& py, int rows, int cols, int n_img, const vo_sift_params& p);
+// View of images [img0, img0 + n) of b: every per-image array shifted (image-major layout).
+SiftBuffers sift_view(const SiftBuffers& b, const Pyramid& py, int img0, int n);
 hipError_t sift_alloc(SiftBuffers& b, const Pyramid& py, int kp_cap, int cand_cap);
 void sift_free(SiftBuffers& b);
 // Enqueue the whole detect+describe pipeline for n_img images (<= allocated).
@@ -167,6 +171,8 @@ struct MatchBuffers {
 #define VO_MATCH_CHUNK 512           // F2 columns per wave task
 
 hipError_t match_alloc(MatchBuffers& b, int max_jobs, int row_cap);
+// View whose job slot 0 is slot k0 of b (partial-result rows of jobs k0, k0+1, ...).
+MatchBuffers match_view(const MatchBuffers& b, int k0);
 void match_free(MatchBuffers& b);
 // d_jobs: device array of n_jobs jobs (prepared once per context); job k uses
 // partial-result slot k.

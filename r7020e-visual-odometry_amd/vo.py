@@ -89,7 +89,7 @@ EXPORTS = [
     "vo_set_calib", "vo_last_error", "vo_sift", "vo_match", "vo_track", "vo_triangulate", "vo_estworldpose",
     "vo_landmarks", "vo_step", "vo_step_batch", "vo_step_batch_dev", "vo_get_landmarks", "vo_reset",
     "vo_sift_match_batch_dev", "vo_fetch_keypoints", "vo_fetch_stereo_pairs", "vo_stream", "vo_set_profiling",
-    "vo_kernel_times", "vo_set_frame_index",
+    "vo_kernel_times", "vo_set_frame_index", "vo_set_concurrency",
 ]
 
 _lib = None
@@ -145,6 +145,7 @@ def load_library(path: str | os.PathLike | None = None):
     L.vo_stream.argtypes = [vp]
     L.vo_stream.restype = vp
     L.vo_set_profiling.argtypes = [vp, C.c_int]
+    L.vo_set_concurrency.argtypes = [vp, C.c_int]
     L.vo_kernel_times.argtypes = [vp, P(C.c_char_p), P(C.c_double), P(C.c_int), C.c_int, P(C.c_int)]
     _lib = L
     return L
@@ -354,6 +355,10 @@ class Context:
     # ---- profiling ----
     def set_profiling(self, on: bool):
         self._check(self.lib.vo_set_profiling(self.h, 1 if on else 0))
+
+    def set_concurrency(self, n_streams: int):
+        """Split batch calls over n_streams (1..4) forked HIP streams; results unchanged."""
+        self._check(self.lib.vo_set_concurrency(self.h, int(n_streams)))
 
     def kernel_times(self) -> dict:
         n = C.c_int(0)

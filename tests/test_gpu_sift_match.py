@@ -56,3 +56,30 @@ def test_match_host_bit_exact(vo, oracle):
     ref = oracle.match(F1, F2)
     assert len(ref) > 100
     assert np.array_equal(got, ref)
+
+
+def test_stream_concurrency_is_invisible(vo, syn):
+    """Splitting a batch over 1, 2, 3 or 4 forked streams gives identical results."""
+    import torch
+    B = 5
+    L, R = syn.independent_pairs(B)
+    dl = torch.from_numpy(L).cuda()
+    dr = torch.from_numpy(R).cuda()
+    torch.cuda.synchronize()
+    ctx = vo.Context(375, 1242, B)
+    ref = None
+    for n in (1, 2, 3, 4):
+        ctx.set_concurrency(n)
+        stats = ctx.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), B)
+        got = [stats]
+        for f in range(B):
+            for i in (2 * f, 2 * f + 1):
+                k, d = ctx.fetch_keypoints(i)
+                got.append((k.tobytes(), d.tobytes()))
+            got.append(ctx.fetch_stereo_pairs(f).tobytes())
+        if ref is None:
+            ref = got
+        else:
+            assert got == ref, n
+    with pytest.raises(Exception):
+        ctx.set_concurrency(0)
