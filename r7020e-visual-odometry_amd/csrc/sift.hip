@@ -1318,6 +1318,17 @@ __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, con
                     jlo = max(jlo, (int)floor(a) - 2); jhi = min(jhi, (int)ceil(b) + 2);
                 } else if (fabs(fi * ct) >= lim) { jlo = 1; jhi = 0; }
                 jlo = max(jlo, 1 - px); jhi = min(jhi, cols - 2 - px);
+                // trim the superset to the exact set: the float test below is monotone
+                // in j on each side (rotations of a row are monotone float sequences),
+                // so the accepted columns form one interval inside [jlo, jhi]
+                const float fi_s = (float)i * sin_t, fi_c = (float)i * cos_t;
+                auto inside = [&](int j) {
+                    const float cr = (float)j * cos_t - fi_s, rr2 = (float)j * sin_t + fi_c;
+                    const float rb = rr2 + (float)(DW / 2) - 0.5f, cb = cr + (float)(DW / 2) - 0.5f;
+                    return rb > -1.0f && rb < (float)DW && cb > -1.0f && cb < (float)DW;
+                };
+                while (jlo <= jhi && !inside(jlo)) ++jlo;
+                while (jhi >= jlo && !inside(jhi)) --jhi;
             }
             rlo[rr] = jlo;
             rlen[rr] = jhi >= jlo ? jhi - jlo + 1 : 0;
@@ -1343,28 +1354,21 @@ __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, con
             float crot[U], rrot[U], gdx[U], gdy[U];
             bool ok[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {                // phase 1: indices, exact validity test, gradient loads
+            for (int u = 0; u < U; ++u) {                // phase 1: indices and gradient loads (every listed sample is valid)
                 const int s = s0 + 64 * u;
-                ok[u] = false; crot[u] = 0.0f; rrot[u] = 0.0f; gdx[u] = 0.0f; gdy[u] = 0.0f;
-                if (s < nsamp) {
-                    while (rstart[lo + 1] <= s) ++lo;
-                    const int i = lo - radius, j = rlo[lo] + (s - rstart[lo]);
-                    const float c_rot = (float)j * cos_t - (float)i * sin_t;
-                    const float r_rot = (float)j * sin_t + (float)i * cos_t;
-                    const float rbin = r_rot + (float)(DW / 2) - 0.5f;
-                    const float cbin = c_rot + (float)(DW / 2) - 0.5f;
-                    const int r = pyy + i, c = px + j;
-                    if (rbin > -1.0f && rbin < (float)DW && cbin > -1.0f && cbin < (float)DW &&
-                        r > 0 && r < rows - 1 && c > 0 && c < cols - 1) {
-                        ok[u] = true; crot[u] = c_rot; rrot[u] = r_rot;
-                        gdx[u] = DAT(gim, P, r, c + 1) - DAT(gim, P, r, c - 1);
-                        gdy[u] = DAT(gim, P, r - 1, c) - DAT(gim, P, r + 1, c);
-                    }
-                }
+                ok[u] = s < nsamp;
+                const int sc = ok[u] ? s : nsamp - 1;
+                while (rstart[lo + 1] <= sc) ++lo;
+                const int i = lo - radius, j = rlo[lo] + (sc - rstart[lo]);
+                crot[u] = (float)j * cos_t - (float)i * sin_t;
+                rrot[u] = (float)j * sin_t + (float)i * cos_t;
+                const int r = pyy + i, c = px + j;
+                gdx[u] = DAT(gim, P, r, c + 1) - DAT(gim, P, r, c - 1);
+                gdy[u] = DAT(gim, P, r - 1, c) - DAT(gim, P, r + 1, c);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {                // phase 2: weights, bins, fixed-point LDS atomics
-                if (!ok[u]) continue;
+                if (ok[u]) {
                 const float c_rot = crot[u], r_rot = rrot[u], dx = gdx[u], dy = gdy[u];
                 float rbin = r_rot + (float)(DW / 2) - 0.5f;
                 float cbin = c_rot + (float)(DW / 2) - 0.5f;
@@ -1392,6 +1396,7 @@ __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, con
                 atomicAdd(h + (DW + 2) * (DN + 2) + 1, vo_desc_fx_quant(v_rco101));
                 atomicAdd(h + (DW + 3) * (DN + 2), vo_desc_fx_quant(v_rco110));
                 atomicAdd(h + (DW + 3) * (DN + 2) + 1, vo_desc_fx_quant(v_rco111));
+                }
             }
         }
         __syncthreads();
