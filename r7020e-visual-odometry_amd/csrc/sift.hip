@@ -1084,8 +1084,8 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
 
 // Orientation assignment: one wave per accepted candidate (npk == -1).  Each
 // lane accumulates its samples' fixed-point weights (vo_desc_fx_quant, 2^-10)
-// into a private LDS column hp[bin][lane] (no contention, conflict-free
-// banks); the 36 bins are then summed over the 64 lanes in 64 bits (integer
+// into a private LDS row hp[lane][bin] (no contention; zeroed with 16-B
+// stores); the 36 bins are then summed over the 64 lanes in 64 bits (integer
 // sums: identical to the oracle's sequential total).  Samples are processed 4
 // per lane per iteration with every gradient load issued first.  Smoothing,
 // peak test and interpolation as the oracle.  (A lane's u32 partial of one bin
@@ -1094,7 +1094,8 @@ __global__ __launch_bounds__(64) void k_orient(const Pyramid* __restrict__ py, c
                                                const int* __restrict__ n_cand, CandOut* __restrict__ cout,
                                                int cand_cap, int n_img)
 {
-    __shared__ uint32_t hp[VO_SIFT_ORI_BINS * 64];
+    constexpr int HS = 40;                                // per-lane histogram stride (16-B rows)
+    __shared__ __attribute__((aligned(16))) uint32_t hp[HS * 64];
     __shared__ float tf[VO_SIFT_ORI_BINS];
     __shared__ float hs[VO_SIFT_ORI_BINS];
     const int lane = threadIdx.x;
@@ -1115,9 +1116,11 @@ __global__ __launch_bounds__(64) void k_orient(const Pyramid* __restrict__ py, c
         const int radius = vo_round(VO_SIFT_ORI_RADIUS * scl);
         const float sigw = VO_SIFT_ORI_SIG * scl;
         const float expf_scale = -1.0f / (2.0f * sigw * sigw);
+        typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int b2 = 0; b2 < VO_SIFT_ORI_BINS; ++b2) hp[b2 * 64 + lane] = 0u;
+        for (int b2 = 0; b2 < HS; b2 += 4) *reinterpret_cast<u4_t*>(&hp[lane * HS + b2]) = u4_t{0u, 0u, 0u, 0u};
         const int side = 2 * radius + 1, nsamp = side * side;
+        const float inv_side = 1.0f / (float)side;          // (s + 0.5) * inv_side is exact enough to floor (s < 2^22)
         constexpr int U = 4;
         for (int s0 = lane; s0 < nsamp; s0 += 64 * U) {
             float gx[U], gy[U];
@@ -1126,19 +1129,20 @@ __global__ __launch_bounds__(64) void k_orient(const Pyramid* __restrict__ py, c
 #pragma unroll
             for (int q = 0; q < U; ++q) {                 // indices, bounds, gradient loads
                 const int s = s0 + 64 * q;
-                const int i = s / side - radius, j = s - (s / side) * side - radius;
+                const int iq = (int)(((float)s + 0.5f) * inv_side);
+                const int i = iq - radius, j = s - iq * side - radius;
                 const int y = r + i, x = c + j;
                 ii[q] = i; jj[q] = j;
                 okk[q] = s < nsamp && y > 0 && y < rows - 1 && x > 0 && x < cols - 1;
-                gx[q] = 0.0f; gy[q] = 0.0f;
-                if (okk[q]) {
-                    gx[q] = DAT(gim, P, y, x + 1) - DAT(gim, P, y, x - 1);
-                    gy[q] = DAT(gim, P, y - 1, x) - DAT(gim, P, y + 1, x);
-                }
+                // every lane loads (clamped to the interior, weight masked below): no branches,
+                // 32-bit offsets from the wave-uniform plane base
+                const int yc = min(max(y, 1), rows - 2), xc = min(max(x, 1), cols - 2);
+                const uint32_t o = (uint32_t)(yc * P + xc);
+                gx[q] = gim[o + 1] - gim[o - 1];
+                gy[q] = gim[o - P] - gim[o + P];
             }
 #pragma unroll
             for (int q = 0; q < U; ++q) {
-                if (!okk[q]) continue;
                 const float dx = gx[q], dy = gy[q];
                 float w = vo_expf((float)(ii[q] * ii[q] + jj[q] * jj[q]) * expf_scale);
                 float mag = sqrtf(dx * dx + dy * dy);
@@ -1146,13 +1150,14 @@ __global__ __launch_bounds__(64) void k_orient(const Pyramid* __restrict__ py, c
                 int bin = vo_round((float)VO_SIFT_ORI_BINS / 360.0f * ori);
                 if (bin >= VO_SIFT_ORI_BINS) bin -= VO_SIFT_ORI_BINS;
                 if (bin < 0) bin += VO_SIFT_ORI_BINS;
-                hp[bin * 64 + lane] += vo_desc_fx_quant((w * mag) * VO_DESC_FX_SCALE);   // private column
+                const uint32_t qv = vo_desc_fx_quant((w * mag) * VO_DESC_FX_SCALE);
+                hp[lane * HS + bin] += okk[q] ? qv : 0u;          // private row; masked samples add 0
             }
         }
         __syncthreads();
         if (lane < VO_SIFT_ORI_BINS) {
-            uint64_t acc = 0;                             // skewed walk: lanes hit distinct banks
-            for (int q = 0; q < 64; ++q) acc += hp[lane * 64 + ((q + lane) & 63)];
+            uint64_t acc = 0;                             // bin = lane: consecutive words per step
+            for (int q = 0; q < 64; ++q) acc += hp[q * HS + lane];
             tf[lane] = vo_hist_fx_to_float(acc);
         }
         __syncthreads();
@@ -1362,9 +1367,9 @@ __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, con
                 const int i = lo - radius, j = rlo[lo] + (sc - rstart[lo]);
                 crot[u] = (float)j * cos_t - (float)i * sin_t;
                 rrot[u] = (float)j * sin_t + (float)i * cos_t;
-                const int r = pyy + i, c = px + j;
-                gdx[u] = DAT(gim, P, r, c + 1) - DAT(gim, P, r, c - 1);
-                gdy[u] = DAT(gim, P, r - 1, c) - DAT(gim, P, r + 1, c);
+                const uint32_t o = (uint32_t)((pyy + i) * P + px + j);   // 32-bit offset from the uniform base
+                gdx[u] = gim[o + 1] - gim[o - 1];
+                gdy[u] = gim[o - P] - gim[o + P];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {                // phase 2: weights, bins, fixed-point LDS atomics
