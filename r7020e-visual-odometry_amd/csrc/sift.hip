@@ -447,11 +447,31 @@ __device__ inline int xcd_remap(int bid, int n)
 __host__ __device__ constexpr int bs_r4(int r) { return (r + 3) & ~3; }
 __host__ __device__ constexpr int bs_rw(int r) { return BS_W + 2 * bs_r4(r); }
 
-template <int RAD, bool EDGE>
+// u8 source of the octave-0 base level (TAG & 4): the x2 upsample is formed
+// while staging each input row, from raw source words prefetched like floats.
+struct U8Src { const uint8_t* p; int ld, rows, cols; };
+
+__device__ __forceinline__ vo_f4 up4_from_words(uint32_t a0, uint32_t a1, uint32_t sa, uint32_t b0, uint32_t b1, uint32_t sb)
+{
+    // 4 source bytes (columns g2-1 .. g2+2) of rows ya, yb -> outputs x .. x+3 (x = 2*g2), as up_sample
+    const uint32_t ba = __builtin_amdgcn_alignbyte(a1, a0, sa), bb = __builtin_amdgcn_alignbyte(b1, b0, sb);
+    float r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int xa = 1 + (i >> 1), xb = (i & 1) ? xa + 1 : xa - 1;
+        const float ha = 0.75f * (float)((ba >> (8 * xa)) & 0xff) + 0.25f * (float)((ba >> (8 * xb)) & 0xff);
+        const float hb = 0.75f * (float)((bb >> (8 * xa)) & 0xff) + 0.25f * (float)((bb >> (8 * xb)) & 0xff);
+        r[i] = 0.75f * ha + 0.25f * hb;
+    }
+    return vo_f4{r[0], r[1], r[2], r[3]};
+}
+
+template <int RAD, bool EDGE, int TAG>
 __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, int pitch, int R, int C,
                                                  float* __restrict__ g_out, const Kern& K,
-                                                 int x0, int y0, int TH, float* rb)
+                                                 int x0, int y0, int TH, float* rb, const U8Src& u8)
 {
+    constexpr bool UP = (TAG & 4) != 0;
     constexpr int P = BS_P;                                // prefetch depth = steps per loop block
     constexpr int R4 = bs_r4(RAD);                         // halo rounded to whole float4s
     constexpr int NQ = 1 + R4 / 2;                         // float4 reads per lane window
@@ -481,18 +501,36 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
     for (int j = 0; j <= RAD; ++j) k[j] = K.k[j];
 
     vo_f4 pf[P], ph[P];
+    typedef uint32_t u2_t __attribute__((ext_vector_type(2)));
+    u2_t pw[UP && !EDGE ? P : 1][4];                       // UP: raw words (ya main, yb main, ya halo, yb halo)
     vo_f2 H[NR][2];
+    // UP: source byte column of the first of the 4 bytes feeding outputs xl.. / hx..
+    const int gm = (xl >> 1) - 1, gh = (hx >> 1) - 1;
 
     // loads for step kk into prefetch slot SL: input row y0-r-E+kk (reflected)
 #define VO_BS_LOAD(KK, SL)                                                                        \
     do {                                                                                          \
-        const float* rowp_ = sp + (size_t)vo_reflect101(y0 - RAD - E + (KK), R) * pitch;          \
-        if (!EDGE) {                                                                              \
-            pf[SL] = *reinterpret_cast<const vo_f4*>(rowp_ + xl);                                 \
-            ph[SL] = *reinterpret_cast<const vo_f4*>(rowp_ + hx);                                 \
+        const int yin_ = vo_reflect101(y0 - RAD - E + (KK), R);                                   \
+        if (UP) {                                                                                 \
+            if (!EDGE) {                                                                          \
+                const int ya_ = yin_ >> 1;                                                        \
+                const int yb_ = (yin_ & 1) ? min(ya_ + 1, u8.rows - 1) : max(ya_ - 1, 0);         \
+                const uint8_t* ra_ = u8.p + (size_t)ya_ * u8.ld;                                  \
+                const uint8_t* rb_ = u8.p + (size_t)yb_ * u8.ld;                                  \
+                pw[SL][0] = *reinterpret_cast<const u2_t*>((uintptr_t)(ra_ + gm) & ~(uintptr_t)3); \
+                pw[SL][1] = *reinterpret_cast<const u2_t*>((uintptr_t)(rb_ + gm) & ~(uintptr_t)3); \
+                pw[SL][2] = *reinterpret_cast<const u2_t*>((uintptr_t)(ra_ + gh) & ~(uintptr_t)3); \
+                pw[SL][3] = *reinterpret_cast<const u2_t*>((uintptr_t)(rb_ + gh) & ~(uintptr_t)3); \
+            }                                                                                     \
         } else {                                                                                  \
-            pf[SL] = vo_f4{rowp_[cm[0]], rowp_[cm[1]], rowp_[cm[2]], rowp_[cm[3]]};               \
-            ph[SL] = vo_f4{rowp_[ch[0]], rowp_[ch[1]], rowp_[ch[2]], rowp_[ch[3]]};               \
+            const float* rowp_ = sp + (size_t)yin_ * pitch;                                       \
+            if (!EDGE) {                                                                          \
+                pf[SL] = *reinterpret_cast<const vo_f4*>(rowp_ + xl);                             \
+                ph[SL] = *reinterpret_cast<const vo_f4*>(rowp_ + hx);                             \
+            } else {                                                                              \
+                pf[SL] = vo_f4{rowp_[cm[0]], rowp_[cm[1]], rowp_[cm[2]], rowp_[cm[3]]};           \
+                ph[SL] = vo_f4{rowp_[ch[0]], rowp_[ch[1]], rowp_[ch[2]], rowp_[ch[3]]};           \
+            }                                                                                     \
         }                                                                                         \
     } while (0)
 
@@ -504,8 +542,25 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
             constexpr int u = decltype(uc)::value;
             const int kk = kk0 + u;
             float* const row = rb;
-            *reinterpret_cast<vo_f4*>(row + R4 + 4 * lane) = pf[u];
-            *reinterpret_cast<vo_f4*>(hpos >= 0 ? row + hpos : dummy) = ph[u];
+            vo_f4 vm = pf[u], vh = ph[u];
+            if constexpr (UP) {
+                const int yin = vo_reflect101(y0 - RAD - E + kk, R);
+                if constexpr (!EDGE) {
+                    const int ya = yin >> 1, yb = (yin & 1) ? min(ya + 1, u8.rows - 1) : max(ya - 1, 0);
+                    const uintptr_t pb = reinterpret_cast<uintptr_t>(u8.p);   // byte misalignment incl. the image base
+                    const uint32_t sa = (uint32_t)((pb + (size_t)ya * u8.ld + gm) & 3), sb = (uint32_t)((pb + (size_t)yb * u8.ld + gm) & 3);
+                    const uint32_t ha = (uint32_t)((pb + (size_t)ya * u8.ld + gh) & 3), hb = (uint32_t)((pb + (size_t)yb * u8.ld + gh) & 3);
+                    vm = up4_from_words(pw[u][0].x, pw[u][0].y, sa, pw[u][1].x, pw[u][1].y, sb);
+                    vh = up4_from_words(pw[u][2].x, pw[u][2].y, ha, pw[u][3].x, pw[u][3].y, hb);
+                } else {                                  // border strips: reflected columns, loads in place
+                    vm = vo_f4{up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, cm[0]), up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, cm[1]),
+                               up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, cm[2]), up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, cm[3])};
+                    vh = vo_f4{up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, ch[0]), up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, ch[1]),
+                               up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, ch[2]), up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, ch[3])};
+                }
+            }
+            *reinterpret_cast<vo_f4*>(row + R4 + 4 * lane) = vm;
+            *reinterpret_cast<vo_f4*>(hpos >= 0 ? row + hpos : dummy) = vh;
             __syncthreads();                              // one-wave block: orders the LDS rows only
             VO_BS_LOAD(kk + P, u);
             float w[4 * NQ];
@@ -537,7 +592,8 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                 const vo_f4 g4 = vo_f4{o[0].x, o[0].y, o[1].x, o[1].y};
                 // columns >= C land in the row padding (pitch is a whole number of strips)
                 const size_t off = (size_t)(y0 + kk - F) * pitch + xl;
-                __builtin_nontemporal_store(g4, reinterpret_cast<vo_f4*>(g_out + off));
+                if (TAG & 2) *reinterpret_cast<vo_f4*>(g_out + off) = g4;            // cached store variant
+                else __builtin_nontemporal_store(g4, reinterpret_cast<vo_f4*>(g_out + off));
             }
             __syncthreads();
         });
@@ -553,10 +609,12 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
 #undef VO_BS_LOAD
 }
 
-template <int RAD, int TAG>   // TAG: 0 level blur, 1 octave-0 base (distinct symbol for the profilers)
+// TAG: 0 level blur, 1 octave-0 base from a float plane, 5 octave-0 base with the x2
+// upsample of the u8 image fused (isrc), 2 cached-store variant (experiments)
+template <int RAD, int TAG>
 __global__ __launch_bounds__(64, RAD <= 6 ? 3 : 2) void k_blur_stream(const float* __restrict__ src, size_t splane, size_t dplane,
                                                     int pitch, int R, int C, float* __restrict__ g_out, Kern K,
-                                                    int n_strips, int n_bands, int TH)
+                                                    int n_strips, int n_bands, int TH, ImageSrc isrc, int in_rows, int in_cols)
 {
     constexpr int R4 = bs_r4(RAD);
     __shared__ __attribute__((aligned(16))) float rb[bs_rw(RAD) + 256];   // staged row + per-lane dummy halo slots
@@ -565,10 +623,17 @@ __global__ __launch_bounds__(64, RAD <= 6 ? 3 : 2) void k_blur_stream(const floa
     const int band = tb % n_bands, img = tb / n_bands;
     const int x0 = strip * BS_W, y0 = min(band * TH, R - TH);
     const size_t os = img * splane, od = img * dplane;
-    if (x0 - R4 < 0 || x0 + BS_W + R4 > C)
-        blur_stream_body<RAD, true>(src + os, pitch, R, C, g_out + od, K, x0, y0, TH, rb);
+    U8Src u8{nullptr, 0, in_rows, in_cols};
+    int margin = 0;
+    if (TAG & 4) {
+        u8.p = ((img & 1) ? isrc.right : isrc.left) + (size_t)(img >> 1) * isrc.frame_stride;
+        u8.ld = isrc.ld;
+        margin = 16;                                       // 8-B word loads stay inside the source row
+    }
+    if (x0 - R4 < 0 || x0 + BS_W + R4 + margin > C)
+        blur_stream_body<RAD, true, TAG>(src + os, pitch, R, C, g_out + od, K, x0, y0, TH, rb, u8);
     else
-        blur_stream_body<RAD, false>(src + os, pitch, R, C, g_out + od, K, x0, y0, TH, rb);
+        blur_stream_body<RAD, false, TAG>(src + os, pitch, R, C, g_out + od, K, x0, y0, TH, rb, u8);
 }
 
 // next octave base.  grid over outputs
@@ -1485,12 +1550,19 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
         if (R >= TH) {
             const int n_bands = (R + TH - 1) / TH;
             const int blocks = n_strips * n_bands * (int)grid.z;
-            if (name[7] == 'b')      // "k_blur_base"
+            static const int cached = getenv("VO_BLUR_CACHED") ? atoi(getenv("VO_BLUR_CACHED")) : 0;
+            if (name[7] == 'b' && src == nullptr)      // "k_blur_base" from the u8 image (x2 upsample fused)
+                VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, 5>), dim3(blocks), dim3(64), 0, s, src, plane, dplane, pitch, R,
+                                C, g, K, n_strips, n_bands, TH, isrc, in_rows, in_cols);
+            else if (name[7] == 'b')
                 VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, 1>), dim3(blocks), dim3(64), 0, s, src, plane, dplane, pitch, R,
-                                C, g, K, n_strips, n_bands, TH);
+                                C, g, K, n_strips, n_bands, TH, isrc, in_rows, in_cols);
+            else if (cached)
+                VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, 2>), dim3(blocks), dim3(64), 0, s, src, plane, dplane, pitch, R,
+                                C, g, K, n_strips, n_bands, TH, isrc, in_rows, in_cols);
             else
                 VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, 0>), dim3(blocks), dim3(64), 0, s, src, plane, dplane, pitch, R,
-                                C, g, K, n_strips, n_bands, TH);
+                                C, g, K, n_strips, n_bands, TH, isrc, in_rows, in_cols);
             return;
         }
     }
@@ -1577,14 +1649,23 @@ void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_
         if (o == 0) {
             Kern K0 = make_kern(py, 0);
             const int rows = p.upsample ? R / 2 : R, cols = p.upsample ? C / 2 : C;
-            // u8 (x2 upsampled) -> float source plane in the scratch buffer, then the level-0 blur
-            const dim3 qg((g.pitch / 4 + 255) / 256, R, n_img);
-            if (p.upsample)
-                VO_LAUNCH(k_base_src<true>, qg, dim3(256), 0, s, src, rows, cols, b.tmp, g.plane, g.pitch, R, C, n_img);
-            else
-                VO_LAUNCH(k_base_src<false>, qg, dim3(256), 0, s, src, rows, cols, b.tmp, g.plane, g.pitch, R, C, n_img);
-            launch_blur<0>(gf, s, b.tmp, g.plane, py.istride, g.pitch, R, C, A + g.g_off[0], nullptr, K0, src, 0, 0,
-                           "k_blur_base");
+            static const bool split = getenv("VO_BASE_SPLIT") != nullptr || getenv("VO_BLUR_PIPE") != nullptr;
+            const int r0 = K0.r;
+            const bool stream_r = r0 == 5 || r0 == 6 || r0 == 8 || r0 == 10 || r0 == 13;
+            if (p.upsample && stream_r && R >= 64 && !split) {
+                // level-0 blur straight from the u8 image, x2 upsample formed while staging rows
+                launch_blur<0>(gf, s, nullptr, 0, py.istride, g.pitch, R, C, A + g.g_off[0], nullptr, K0, src, rows, cols,
+                               "k_blur_base");
+            } else {
+                // u8 (x2 upsampled) -> float source plane in the scratch buffer, then the level-0 blur
+                const dim3 qg((g.pitch / 4 + 255) / 256, R, n_img);
+                if (p.upsample)
+                    VO_LAUNCH(k_base_src<true>, qg, dim3(256), 0, s, src, rows, cols, b.tmp, g.plane, g.pitch, R, C, n_img);
+                else
+                    VO_LAUNCH(k_base_src<false>, qg, dim3(256), 0, s, src, rows, cols, b.tmp, g.plane, g.pitch, R, C, n_img);
+                launch_blur<0>(gf, s, b.tmp, g.plane, py.istride, g.pitch, R, C, A + g.g_off[0], nullptr, K0, src, 0, 0,
+                               "k_blur_base");
+            }
         } else {
             const OctGeom& pg = py.oct[o - 1];
             size_t n = (size_t)n_img * R * C;

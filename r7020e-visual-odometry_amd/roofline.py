@@ -48,8 +48,7 @@ def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3) -> dict:
         out[name] = (b + nbytes, l + launches)
 
     R0, C0 = dims[0]
-    add("k_base_src<true>", n_img * (rows * cols + 4 * R0 * C0), 1)      # u8 in, x2-upsampled float plane out
-    add("k_blur_base", n_img * 8 * R0 * C0, 1)                            # source plane in, G0 out
+    add("k_blur_base", n_img * (rows * cols + 4 * R0 * C0), 1)           # u8 in (x2 upsample fused), G0 out
     # octaves from o_small on are built by one k_blur_small launch in LDS (planes <= SMALL_PX)
     o_small = next((o for o in range(1, len(dims)) if all(r * c <= SMALL_PX for r, c in dims[o:])), len(dims))
     for o, (R, C) in enumerate(dims):

@@ -83,3 +83,25 @@ def test_stream_concurrency_is_invisible(vo, syn):
             assert got == ref, n
     with pytest.raises(Exception):
         ctx.set_concurrency(0)
+
+
+@pytest.mark.parametrize("offset", [1, 3])
+def test_misaligned_image_pointers(vo, oracle, syn, offset):
+    """Device images at byte offsets (odd row pitch 1242, unaligned base) give the oracle's keypoints."""
+    import torch
+    B = 2
+    L, R = syn.independent_pairs(B)
+    n = L[0].size
+    buf_l = torch.zeros(B * n + 16, dtype=torch.uint8, device="cuda")
+    buf_r = torch.zeros(B * n + 16, dtype=torch.uint8, device="cuda")
+    buf_l[offset:offset + B * n] = torch.from_numpy(L.reshape(-1)).cuda()
+    buf_r[offset:offset + B * n] = torch.from_numpy(R.reshape(-1)).cuda()
+    torch.cuda.synchronize()
+    ctx = vo.Context(375, 1242, B)
+    ctx.sift_match_batch_dev(buf_l.data_ptr() + offset, buf_r.data_ptr() + offset, B)
+    for f in range(B):
+        for img, src in ((2 * f, L[f]), (2 * f + 1, R[f])):
+            k, d = ctx.fetch_keypoints(img)
+            rk, rd = oracle.sift(src)
+            _same_kps(k, rk)
+            assert np.array_equal(d, rd)
