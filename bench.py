@@ -11,7 +11,8 @@ scaling, no data-path collective; value = all frames / max-over-ranks time.
 Prints ONE JSON line (rank 0) with the driver's contract fields plus
 `roofline` (dominant kernel, HIP-event durations measured in this process)
 and `cpu_baseline` (the CPU oracle on a bounded sample, rank 0 at N=1).
-`--full` additionally times the full per-frame path (vo_step_batch).
+`full_path` additionally times the full per-frame path (vo_step_batch_dev) over
+a synthetic moving-camera sequence (--full-frames, default 64; 0 skips).
 """
 from __future__ import annotations
 
@@ -44,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=10, help="frames in the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3)
+    ap.add_argument("--full-frames", type=int, default=64,
+                    help="frames of the synthetic sequence timed through the full per-frame path (0: skip)")
     return ap.parse_args()
 
 
@@ -126,6 +129,55 @@ def main():
     roof["pyramid_model_gbs"] = pyr_bytes / (pyr_ms * 1e-3) / 1e9 if pyr_ms > 0 else None
     roof["kernel_ms_per_step"] = {n: round(v[0] / args.profile_steps, 4) for n, v in sorted(kt.items(), key=lambda kv: -kv[1][0])}
 
+    # ---- BASELINE configs[2] on synthetic data: the full per-frame path (SIFT x2, stereo
+    # match, tracking matches, DLT, P3P+MSAC 2048 hypotheses, landmarks) over a moving-camera
+    # sequence, frames chained across batches of B (device-resident inputs) ----
+    full = None
+    if args.full_frames > 0:
+        nf = args.full_frames // B * B
+        # ping-pong walk (0.25 m/frame forward, then back) keeps the fronto-parallel planes
+        # of the synthetic scene in view, so keypoint counts stay near the ~2k of configs[1]
+        half = (nf + 1) // 2
+        SL, SR, _gt = syn.sequence(half, ROWS, COLS, seed=syn.SEED_BASE + 0x100 * rank, step_m=0.25, yaw_deg=0.1)
+        SL = np.ascontiguousarray(np.concatenate([SL, SL[::-1]])[:nf])
+        SR = np.ascontiguousarray(np.concatenate([SR, SR[::-1]])[:nf])
+        d_sl = torch.from_numpy(SL).to(f"cuda:{local}")
+        d_sr = torch.from_numpy(SR).to(f"cuda:{local}")
+        P1, P2 = syn.calib()
+        fctx = vo.Context(ROWS, COLS, B, device=local, calib=vo.calib_from(P1, P2))
+        fs = SL[0].size
+
+        def run_seq():
+            fctx.reset()
+            outs = []
+            for b0 in range(0, nf, B):
+                outs.append(fctx.step_batch_dev(d_sl.data_ptr() + b0 * fs, d_sr.data_ptr() + b0 * fs, B))
+            return np.concatenate(outs)
+
+        run_seq()
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        reps = 2
+        for _ in range(reps):
+            outs = run_seq()
+        torch.cuda.synchronize()
+        fel = time.perf_counter() - t0
+        barrier()
+        if dist is not None:
+            t = torch.tensor([fel], device=f"cuda:{local}", dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            fel = float(t.item())
+        ok = outs["status"][1:] == 0
+        full = {"metric": "stereo frames/sec, full per-frame path (BASELINE configs[2] on synthetic sequence)",
+                "value": nf * reps * world / fel, "unit": "stereo frames/s", "frames_per_rank": nf, "batch": B,
+                "ransac_hypotheses": 2048, "frames_with_pose": int(ok.sum()), "mean_inliers": float(outs["n_inliers"][1:].mean()),
+                "mean_keypoints_per_image": float((outs["n_left"] + outs["n_right"]).mean() / 2),
+                "note": "frames chained through vo_step_batch_dev (tracking carried across batches); "
+                        "includes the per-batch pose/landmark download and host pose chain"}
+        fctx.close()
+        del d_sl, d_sr
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle
@@ -153,6 +205,7 @@ def main():
                        "parallelism": f"frames sharded over {world} GPU(s)"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "full_path": full,
         }
         print(json.dumps(line))
     if dist is not None:
