@@ -234,17 +234,9 @@ VO_HD vo_u32x4 vo_philox4x32_10(vo_u32x4 ctr, uint32_t k0, uint32_t k1)
 VO_HD uint32_t vo_rand_index(uint32_t r, uint32_t n) { return (uint32_t)(((uint64_t)r * n) >> 32); }
 
 /* ------------------------------------------------------------------------ */
-/* Fixed-point histogram accumulation.  Orientation and descriptor          */
-/* histograms are summed in 2^-20 fixed point (int64): integer addition is  */
-/* associative, so the GPU may add contributions in any order (LDS atomics) */
-/* and still equal the oracle's serial loop bit for bit.  A contribution v  */
-/* (>= 0, <= 2^11) quantises to rint(v * 2^20); a bin converts back through */
-/* double (exact) to float (one correct rounding).                           */
-/* ------------------------------------------------------------------------ */
-#define VO_FX_SCALE 1048576.0f
-VO_HD int32_t vo_fx_quant(float v) { return (int32_t)rintf(v * VO_FX_SCALE); }
-VO_HD float vo_fx_to_float(int64_t s) { return (float)((double)s * (1.0 / 1048576.0)); }
-
+/* Fixed-point histogram accumulation.  Integer addition is associative, so  */
+/* the GPU may add contributions in any order (LDS atomics, per-lane rows,   */
+/* several copies) and still equal the oracle's serial loop bit for bit.     */
 /* Orientation and descriptor histograms: unsigned 32-bit fixed point at     */
 /* 2^-10.  A weight v >= 0 is pre-scaled by 2^10 (exact: a power of two) and  */
 /* enters as rintf(v).  Overflow-free by construction, |dI| <= 255 so one     */
@@ -253,6 +245,8 @@ VO_HD float vo_fx_to_float(int64_t s) { return (float)((double)s * (1.0 / 104857
 /*    5.5e3 samples once the radius is capped at VO_SIFT_DESCR_RMAX           */
 /*    (hist_width <= 36.3): < 2.1e9 < 2^32;                                   */
 /*  - orientation: bins are summed in 64 bits (any window size).              */
+/* A bin converts back with one correct rounding: (float)sum * 2^-10.        */
+/* ------------------------------------------------------------------------ */
 #define VO_DESC_FX_SCALE 1024.0f
 VO_HD uint32_t vo_desc_fx_quant(float v_scaled) { return (uint32_t)rintf(v_scaled); }
 VO_HD float vo_desc_fx_to_float(uint32_t s) { return (float)s * (1.0f / VO_DESC_FX_SCALE); }
