@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16, help="stereo frames per step")
+    ap.add_argument("--batch", type=int, default=32, help="stereo frames per step")
     ap.add_argument("--cpu-frames", type=int, default=10, help="frames in the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3)

@@ -225,11 +225,16 @@ int vo_fetch_stereo_pairs(vo_ctx* ctx, int frame, uint32_t* pairs, int capacity,
 void* vo_stream(vo_ctx* ctx);
 int vo_set_profiling(vo_ctx* ctx, int enable);
 
-/* Batch calls (vo_sift_match_batch_dev, vo_step_batch*) split their frames over
- * n_streams (1..4, default 2) HIP streams forked from / joined into vo_stream(),
- * so latency-bound stages of one part overlap bandwidth-bound stages of
- * another.  Results are identical for any n_streams.  While profiling is on,
- * batches run as one part (clean per-kernel durations). */
+/* Batch calls run SIFT in two phases on two internal streams forked from
+ * vo_stream(): the scale space (bandwidth-bound) and the feature stages +
+ * stereo matching (latency-bound).  vo_set_concurrency(n) additionally splits a
+ * batch into n parts (1..4, default 1) so the features of part k overlap the
+ * scale space of part k+1.  vo_sift_match_batch_dev without stats is
+ * asynchronous: consecutive calls alternate between two buffer sets, so the
+ * scale space of call N+1 overlaps the feature stages of call N; inputs are
+ * read after earlier work on vo_stream() and must stay valid until the call
+ * completes (vo_fetch_* / any synchronising call wait for it).  Results are
+ * identical for any n and any call pattern. */
 int vo_set_concurrency(vo_ctx* ctx, int n_streams);
 int vo_kernel_times(vo_ctx* ctx, const char** names, double* ms, int* calls, int capacity, int* n);
 

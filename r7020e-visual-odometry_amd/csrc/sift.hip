@@ -1610,8 +1610,8 @@ static void launch_blur(dim3 grid, hipStream_t s, const float* src, size_t plane
     }
 }
 
-void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img, const vo_sift_params& p,
-                  hipStream_t s, const Pyramid* d_py)
+void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img, const vo_sift_params& p,
+                          hipStream_t s, const Pyramid* d_py)
 {
     const int L = py.L;
     float* A = b.arena;
@@ -1692,6 +1692,12 @@ void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_
         default: VO_LAUNCH(k_ext_stream<5>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
         }
     }
+}
+
+void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
+                           const Pyramid* d_py)
+{
+    float* A = b.arena;
     const dim3 gs(py.n_seg > 0 ? py.n_seg : 1, n_img);
     VO_LAUNCH(k_seg_count, gs, dim3(256), 0, s, b.mask, b.woff, py.n_words, py.n_seg);
     VO_LAUNCH(k_seg_scan, dim3(n_img), dim3(1024), 0, s, b.woff, b.n_cand, py.n_seg);
@@ -1703,6 +1709,13 @@ void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_
     VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, b.n_cand, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
                        n_img, p.upsample);
     VO_LAUNCH(k_desc, dim3(8192), dim3(64), 0, s, d_py, A, b.kpi, b.n_kp, b.desc, b.meta, b.kp_cap, n_img);
+}
+
+void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img, const vo_sift_params& p,
+                  hipStream_t s, const Pyramid* d_py)
+{
+    sift_enqueue_pyramid(py, b, src, n_img, p, s, d_py);
+    sift_enqueue_features(py, b, n_img, p, s, d_py);
 }
 
 }  // namespace vo

@@ -66,9 +66,21 @@ struct vo_ctx {
     // fork from / join into `stream` (latency-bound SIFT stages of one part
     // overlap bandwidth-bound stages of another)
     static constexpr int MAX_SUB = 4;
-    int n_sub = 2;
-    hipStream_t sub[MAX_SUB] = {};
+    int n_sub = 1;
+    hipStream_t sub[MAX_SUB] = {};                 // sub[0]: scale-space stream, sub[1]: feature stream
     hipEvent_t ev_fork = nullptr, ev_join[MAX_SUB] = {};
+    // Asynchronous batch pipeline (vo_sift_match_batch_dev): calls alternate between two
+    // buffer sets; set 0 is the context's own buffers (sb, mb, stereo jobs, pairs), set 1
+    // is `aux`.  A call's scale space waits only for the previous use of its own set, so
+    // the pyramid of call N+1 overlaps the latency-bound feature stages of call N.
+    struct AuxSet {
+        SiftBuffers sb;
+        MatchBuffers mb;
+        MatchJob* d_jobs = nullptr;
+        int* pair_i = nullptr; int* pair_j = nullptr; int* pair_n = nullptr;
+    } aux;
+    hipEvent_t ev_done[2] = {};
+    int next_set = 0, last_set = 0;
     Pyramid py;
     Pyramid* d_py = nullptr;
     SiftBuffers sb;                  // 2*max_batch + 2 image slots (last 2 = carried frame)
@@ -142,12 +154,19 @@ static void destroy_streams(vo_ctx* c)
     }
     if (c->ev_fork) hipEventDestroy(c->ev_fork);
     c->ev_fork = nullptr;
+    for (int k = 0; k < 2; ++k) {
+        if (c->ev_done[k]) hipEventDestroy(c->ev_done[k]);
+        c->ev_done[k] = nullptr;
+    }
 }
 
 static void destroy_buffers(vo_ctx* c)
 {
     sift_free(c->sb);
     match_free(c->mb);
+    sift_free(c->aux.sb);
+    match_free(c->aux.mb);
+    hipFree(c->aux.d_jobs); hipFree(c->aux.pair_i); hipFree(c->aux.pair_j); hipFree(c->aux.pair_n);
     geom_free(c->gb);
     hipFree(c->d_py); hipFree(c->d_jobs); hipFree(c->d_pair_i); hipFree(c->d_pair_j); hipFree(c->d_pair_n);
     hipFree(c->d_img); hipFree(c->d_fd[0]); hipFree(c->d_fd[1]); hipFree(c->d_fm[0]); hipFree(c->d_fm[1]);
@@ -189,6 +208,8 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
         if ((e = hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
     }
     if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("event", e);
+    for (int k = 0; k < 2; ++k)
+        if ((e = hipEventCreateWithFlags(&c->ev_done[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
     const int n_slots = 2 * max_batch + 2;
     const int kp_cap = c->sp.max_keypoints;
     build_pyramid_geometry(c->py, rows, cols, n_slots, c->sp);
@@ -234,6 +255,29 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
         J.out_i = c->d_mi; J.out_j = c->d_mj; J.out_n = c->d_mn; J.cap = kp_cap;
     }
     if ((e = hipMemcpy(c->d_jobs, jobs.data(), sizeof(MatchJob) * n_jobs, hipMemcpyHostToDevice)) != hipSuccess) return bail("jobs copy", e);
+    // second buffer set of the asynchronous batch pipeline (stereo frames only)
+    {
+        vo_ctx::AuxSet& X = c->aux;
+        if ((e = sift_alloc(X.sb, c->py, kp_cap, 4 * kp_cap)) != hipSuccess) return bail("sift buffers (set 1)", e);
+        if ((e = match_alloc(X.mb, max_batch, kp_cap)) != hipSuccess) return bail("match buffers (set 1)", e);
+        if ((e = hipMalloc((void**)&X.d_jobs, sizeof(MatchJob) * max_batch)) != hipSuccess) return bail("jobs (set 1)", e);
+        if ((e = hipMalloc((void**)&X.pair_i, sizeof(int) * (size_t)max_batch * kp_cap)) != hipSuccess) return bail("pairs", e);
+        if ((e = hipMalloc((void**)&X.pair_j, sizeof(int) * (size_t)max_batch * kp_cap)) != hipSuccess) return bail("pairs", e);
+        if ((e = hipMalloc((void**)&X.pair_n, sizeof(int) * max_batch)) != hipSuccess) return bail("pairs", e);
+        if ((e = hipMemset(X.pair_n, 0, sizeof(int) * max_batch)) != hipSuccess) return bail("pairs", e);
+        std::vector<MatchJob> xj(max_batch);
+        memset(xj.data(), 0, sizeof(MatchJob) * max_batch);
+        for (int f = 0; f < max_batch; ++f) {
+            MatchJob& J = xj[f];
+            const int il = 2 * f, ir = 2 * f + 1;
+            J.d1 = X.sb.desc + il * dstride; J.m1 = X.sb.meta + (size_t)il * kp_cap; J.idx1 = nullptr; J.n1 = X.sb.n_kp + il;
+            J.d2 = X.sb.desc + ir * dstride; J.m2 = X.sb.meta + (size_t)ir * kp_cap; J.idx2 = nullptr; J.n2 = X.sb.n_kp + ir;
+            J.out_i = X.pair_i + (size_t)f * kp_cap; J.out_j = X.pair_j + (size_t)f * kp_cap; J.out_n = X.pair_n + f;
+            J.cap = kp_cap;
+        }
+        if ((e = hipMemcpy(X.d_jobs, xj.data(), sizeof(MatchJob) * max_batch, hipMemcpyHostToDevice)) != hipSuccess)
+            return bail("jobs copy (set 1)", e);
+    }
     return c;
 }
 
@@ -288,6 +332,7 @@ int vo_kernel_times(vo_ctx* c, const char** names, double* ms, int* calls, int c
 static int finish(vo_ctx* c)
 {
     hipError_t e = hipStreamSynchronize(c->stream);
+    for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipStreamSynchronize(c->sub[k]);
     if (e != hipSuccess) return fail(c, VO_ERR_HIP, "stream sync: %s", hipGetErrorString(e));
     e = hipGetLastError();
     if (e != hipSuccess) return fail(c, VO_ERR_HIP, "launch: %s", hipGetErrorString(e));
@@ -295,11 +340,14 @@ static int finish(vo_ctx* c)
     g_prof = nullptr;
     return VO_OK;
 }
-
-static void begin_call(vo_ctx* c)
+// quiesce: calls that run on `stream` over the context's own buffers first wait for any
+// batch still in flight on either buffer set (no host synchronisation)
+static void begin_call(vo_ctx* c, bool quiesce = true)
 {
     hipSetDevice(c->device);
     g_prof = c->prof.on ? &c->prof : nullptr;
+    if (quiesce)
+        for (int k = 0; k < 2; ++k) hipStreamWaitEvent(c->stream, c->ev_done[k], 0);
 }
 
 int vo_sift(vo_ctx* c, const uint8_t* img, int rows, int cols, int ld, vo_keypoint* kps, uint8_t* desc, int capacity,
@@ -354,50 +402,70 @@ int vo_match(vo_ctx* c, const uint8_t* F1, int n1, const uint8_t* F2, int n2, ui
 }
 
 // SIFT + stereo match on B frames already in device memory.
-static int enqueue_sift_stereo(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B)
+// buffers of set `set` of the asynchronous batch pipeline
+struct SetRef { SiftBuffers* sb; MatchBuffers* mb; MatchJob* jobs; int* pair_i; int* pair_j; int* pair_n; };
+static SetRef set_ref(vo_ctx* c, int set)
+{
+    if (set == 0) return {&c->sb, &c->mb, c->d_jobs + job_stereo(c, 0), c->d_pair_i, c->d_pair_j, c->d_pair_n};
+    return {&c->aux.sb, &c->aux.mb, c->aux.d_jobs, c->aux.pair_i, c->aux.pair_j, c->aux.pair_n};
+}
+
+// SIFT of 2B images + stereo matching of B frames into buffer set `set`.  The frames are
+// split into `parts` (vo_set_concurrency); every part's scale space runs on sub[0] and its
+// feature stages + stereo matching on sub[1] once that part's scale space is done, so the
+// features of part k overlap the scale space of part k+1 (and of the next call, which uses
+// the other set).  Inputs are ordered after earlier work on `stream`; the set's previous
+// contents are released by its ev_done.  With `join`, `stream` waits for the result.
+static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uint8_t* d_r, int B, bool join)
 {
     const size_t fs = (size_t)c->rows * c->cols;
-    // per-kernel profiling wants undisturbed launch durations: one part then
     const int parts = c->prof.on ? 1 : std::min(c->n_sub, B);
-    if (parts <= 1) {
-        ImageSrc src{d_l, d_r, fs, c->cols, 0};
-        sift_enqueue(c->py, c->sb, src, 2 * B, c->sp, c->stream, c->d_py);
-        match_launch(c->mb, c->d_jobs + job_stereo(c, 0), B, c->mp, c->stream);
-        return VO_OK;
-    }
-    // fork: frames [f0, f1) of part p run SIFT + stereo matching on sub[p] over
-    // image-range views of the same buffers (image-major layouts), then join
-    HIPC(c, hipEventRecord(c->ev_fork, c->stream));
+    SetRef S = set_ref(c, set);
+    hipStream_t sp = c->sub[0], st = c->sub[1];
+    HIPC(c, hipEventRecord(c->ev_fork, c->stream));           // inputs / earlier work on `stream`
+    HIPC(c, hipStreamWaitEvent(sp, c->ev_fork, 0));
+    HIPC(c, hipStreamWaitEvent(sp, c->ev_done[set], 0));      // set free (its previous features done)
     for (int p = 0; p < parts; ++p) {
-        const int f0 = B * p / parts, f1 = B * (p + 1) / parts, nf = f1 - f0;
-        hipStream_t s = c->sub[p];
-        HIPC(c, hipStreamWaitEvent(s, c->ev_fork, 0));
+        const int f0 = B * p / parts, nf = B * (p + 1) / parts - f0;
         ImageSrc src{d_l + f0 * fs, d_r + f0 * fs, fs, c->cols, 0};
-        SiftBuffers v = sift_view(c->sb, c->py, 2 * f0, 2 * nf);
-        sift_enqueue(c->py, v, src, 2 * nf, c->sp, s, c->d_py);
-        match_launch(match_view(c->mb, job_stereo(c, f0)), c->d_jobs + job_stereo(c, f0), nf, c->mp, s);
-        HIPC(c, hipEventRecord(c->ev_join[p], s));
-        HIPC(c, hipStreamWaitEvent(c->stream, c->ev_join[p], 0));
+        SiftBuffers v = sift_view(*S.sb, c->py, 2 * f0, 2 * nf);
+        sift_enqueue_pyramid(c->py, v, src, 2 * nf, c->sp, sp, c->d_py);
+        HIPC(c, hipEventRecord(c->ev_join[p], sp));
     }
+    for (int p = 0; p < parts; ++p) {
+        const int f0 = B * p / parts, nf = B * (p + 1) / parts - f0;
+        SiftBuffers v = sift_view(*S.sb, c->py, 2 * f0, 2 * nf);
+        HIPC(c, hipStreamWaitEvent(st, c->ev_join[p], 0));
+        sift_enqueue_features(c->py, v, 2 * nf, c->sp, st, c->d_py);
+        match_launch(match_view(*S.mb, f0), S.jobs + f0, nf, c->mp, st);
+    }
+    HIPC(c, hipEventRecord(c->ev_done[set], st));
+    if (join) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_done[set], 0));
+    c->last_set = set;
     return VO_OK;
 }
 
 int vo_sift_match_batch_dev(vo_ctx* c, const uint8_t* d_lefts, const uint8_t* d_rights, int B, vo_pair_stats* stats)
 {
     if (!c || !d_lefts || !d_rights || B < 1 || B > c->max_batch) return fail(c, VO_ERR_ARG, "vo_sift_match_batch_dev: bad arguments");
-    begin_call(c);
-    enqueue_sift_stereo(c, d_lefts, d_rights, B);
+    begin_call(c, false);
+    const int set = c->next_set;
+    c->next_set ^= 1;
+    const bool sync = stats || c->prof.on;
+    int rc = enqueue_sift_stereo(c, set, d_lefts, d_rights, B, sync);
+    if (rc) return rc;
     c->last_B = B;
-    if (!stats && !c->prof.on) {
+    if (!sync) {
         g_prof = nullptr;
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return fail(c, VO_ERR_HIP, "launch: %s", hipGetErrorString(e));
         return VO_OK;
     }
+    SetRef S = set_ref(c, set);
     std::vector<int> nk(2 * B), np(B);
-    HIPC(c, hipMemcpyAsync(nk.data(), c->sb.n_kp, sizeof(int) * 2 * B, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipMemcpyAsync(np.data(), c->d_pair_n, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
-    int rc = finish(c);
+    HIPC(c, hipMemcpyAsync(nk.data(), S.sb->n_kp, sizeof(int) * 2 * B, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(np.data(), S.pair_n, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
+    rc = finish(c);
     if (rc) return rc;
     if (stats) {
         for (int f = 0; f < B; ++f) {
@@ -413,13 +481,16 @@ int vo_fetch_keypoints(vo_ctx* c, int image, vo_keypoint* kps, uint8_t* desc, in
     if (!c || image < 0 || image >= c->sb.n_img) return fail(c, VO_ERR_ARG, "vo_fetch_keypoints: bad image");
     hipSetDevice(c->device);
     HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipEventSynchronize(c->ev_done[c->last_set]));
+    // batch results live in the last call's buffer set (set 1 holds stereo frames only)
+    const SiftBuffers& B = (c->last_set == 1 && image < 2 * c->max_batch) ? c->aux.sb : c->sb;
     int cnt = 0;
-    HIPC(c, hipMemcpy(&cnt, c->sb.n_kp + image, sizeof(int), hipMemcpyDeviceToHost));
+    HIPC(c, hipMemcpy(&cnt, B.n_kp + image, sizeof(int), hipMemcpyDeviceToHost));
     if (n) *n = cnt;
-    int m = std::min(std::min(cnt, c->sb.kp_cap), capacity);
+    int m = std::min(std::min(cnt, B.kp_cap), capacity);
     if (m > 0) {
-        if (kps) HIPC(c, hipMemcpy(kps, c->sb.kp + (size_t)image * c->sb.kp_cap, sizeof(vo_keypoint) * m, hipMemcpyDeviceToHost));
-        if (desc) HIPC(c, hipMemcpy(desc, c->sb.desc + (size_t)image * c->sb.kp_cap * VO_DESC_LEN, (size_t)m * VO_DESC_LEN, hipMemcpyDeviceToHost));
+        if (kps) HIPC(c, hipMemcpy(kps, B.kp + (size_t)image * B.kp_cap, sizeof(vo_keypoint) * m, hipMemcpyDeviceToHost));
+        if (desc) HIPC(c, hipMemcpy(desc, B.desc + (size_t)image * B.kp_cap * VO_DESC_LEN, (size_t)m * VO_DESC_LEN, hipMemcpyDeviceToHost));
     }
     return VO_OK;
 }
@@ -429,14 +500,16 @@ int vo_fetch_stereo_pairs(vo_ctx* c, int frame, uint32_t* pairs, int capacity, i
     if (!c || frame < 0 || frame >= c->max_batch) return fail(c, VO_ERR_ARG, "vo_fetch_stereo_pairs: bad frame");
     hipSetDevice(c->device);
     HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipEventSynchronize(c->ev_done[c->last_set]));
+    SetRef S = set_ref(c, c->last_set);
     int P = 0;
-    HIPC(c, hipMemcpy(&P, c->d_pair_n + frame, sizeof(int), hipMemcpyDeviceToHost));
+    HIPC(c, hipMemcpy(&P, S.pair_n + frame, sizeof(int), hipMemcpyDeviceToHost));
     if (n) *n = P;
     int m = std::min(P, capacity);
     if (m > 0 && pairs) {
         std::vector<int> ii(m), jj(m);
-        HIPC(c, hipMemcpy(ii.data(), c->d_pair_i + (size_t)frame * c->sb.kp_cap, sizeof(int) * m, hipMemcpyDeviceToHost));
-        HIPC(c, hipMemcpy(jj.data(), c->d_pair_j + (size_t)frame * c->sb.kp_cap, sizeof(int) * m, hipMemcpyDeviceToHost));
+        HIPC(c, hipMemcpy(ii.data(), S.pair_i + (size_t)frame * c->sb.kp_cap, sizeof(int) * m, hipMemcpyDeviceToHost));
+        HIPC(c, hipMemcpy(jj.data(), S.pair_j + (size_t)frame * c->sb.kp_cap, sizeof(int) * m, hipMemcpyDeviceToHost));
         for (int k = 0; k < m; ++k) { pairs[2 * k] = (uint32_t)ii[k] + 1; pairs[2 * k + 1] = (uint32_t)jj[k] + 1; }
     }
     return VO_OK;
@@ -512,7 +585,8 @@ static int run_batch(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B, v
 {
     if (!c->has_calib) return fail(c, VO_ERR_STATE, "vo_step: no calibration (vo_set_calib)");
     const int K = c->sb.kp_cap;
-    enqueue_sift_stereo(c, d_l, d_r, B);
+    int rc0 = enqueue_sift_stereo(c, 0, d_l, d_r, B, true);       // buffer set 0, joined into `stream`
+    if (rc0) return rc0;
     StepArgs a = step_args(c, B);
     geom_enqueue(c->gb, c->mb, c->d_jobs + job_track(c, 0, 0), a, c->mp, c->stream);
     std::vector<FrameGeom> fg(B);

@@ -357,7 +357,7 @@ class Context:
         self._check(self.lib.vo_set_profiling(self.h, 1 if on else 0))
 
     def set_concurrency(self, n_streams: int):
-        """Split batch calls over n_streams (1..4) forked HIP streams; results unchanged."""
+        """Split each batch into n parts (1..4) pipelined over the scale-space and feature streams; results unchanged."""
         self._check(self.lib.vo_set_concurrency(self.h, int(n_streams)))
 
     def kernel_times(self) -> dict:

@@ -1,4 +1,5 @@
-"""Small driver for rocprofv3 counter passes: N batches of the bench workload."""
+"""Small driver for rocprofv3 passes: N batches of the bench workload, issued back to back
+(asynchronous pipeline, like bench.py's timed loop), then one synchronising call."""
 import sys
 from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
@@ -14,6 +15,7 @@ dl, dr = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
 torch.cuda.synchronize()
 ctx = vo.Context(375, 1242, B)
 for _ in range(N):
-    ctx.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), B, stats=True)
+    ctx.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), B, stats=False)
+ctx.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), B, stats=True)
 torch.cuda.synchronize()
 print("done")

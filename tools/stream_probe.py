@@ -1,5 +1,4 @@
-"""Probe: throughput of N libvo contexts (own HIP streams) sharing one GPU, each
-with B frames per call, calls issued back to back without host sync."""
+"""Probe: frames/s of one libvo context vs batch size and vo_set_concurrency."""
 import sys, time
 from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
@@ -8,22 +7,20 @@ import torch
 import vo_amd  # noqa
 from r7020e_visual_odometry_amd import vo, synthetic as syn
 
-for nctx, B in [(1, 16), (2, 8), (2, 16), (4, 8), (1, 32), (1, 64)]:
+for B in (16, 32):
     L, R = syn.independent_pairs(B)
     dl, dr = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
-    ctxs = [vo.Context(375, 1242, B) for _ in range(nctx)]
-    for c in ctxs:
-        c.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), B, stats=False)
-    torch.cuda.synchronize()
-    steps = 10
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        for c in ctxs:
-            c.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), B, stats=False)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    print(f"ctx={nctx} B={B}: {nctx * B * steps / dt:.0f} frames/s", flush=True)
-    for c in ctxs:
-        c.close()
-    del dl, dr
-    torch.cuda.empty_cache()
+    ctx = vo.Context(375, 1242, B)
+    for ns in (1, 2, 3, 4):
+        ctx.set_concurrency(ns)
+        for _ in range(2):
+            ctx.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), B, stats=False)
+        torch.cuda.synchronize()
+        steps = 10
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ctx.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), B, stats=False)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        print(f"B={B} streams={ns}: {B * steps / dt:.0f} frames/s", flush=True)
+    ctx.close()
