@@ -315,9 +315,16 @@ int vo_set_profiling(vo_ctx* c, int enable)
     return VO_OK;
 }
 
+static int finish(vo_ctx* c);
 int vo_kernel_times(vo_ctx* c, const char** names, double* ms, int* calls, int capacity, int* n)
 {
     if (!c) return VO_ERR_ARG;
+    hipSetDevice(c->device);
+    if (c->prof.on) {                                  // asynchronous calls may still be in flight
+        g_prof = &c->prof;
+        int rc = finish(c);
+        if (rc) return rc;
+    }
     int m = (int)c->prof.names.size();
     if (n) *n = m;
     for (int i = 0; i < m && i < capacity; ++i) {
@@ -419,7 +426,7 @@ static SetRef set_ref(vo_ctx* c, int set)
 static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uint8_t* d_r, int B, bool join)
 {
     const size_t fs = (size_t)c->rows * c->cols;
-    const int parts = c->prof.on ? 1 : std::min(c->n_sub, B);
+    const int parts = std::min(c->n_sub, B);
     SetRef S = set_ref(c, set);
     hipStream_t sp = c->sub[0], st = c->sub[1];
     HIPC(c, hipEventRecord(c->ev_fork, c->stream));           // inputs / earlier work on `stream`
@@ -451,7 +458,7 @@ int vo_sift_match_batch_dev(vo_ctx* c, const uint8_t* d_lefts, const uint8_t* d_
     begin_call(c, false);
     const int set = c->next_set;
     c->next_set ^= 1;
-    const bool sync = stats || c->prof.on;
+    const bool sync = stats != nullptr;      // profiling events are collected by vo_kernel_times
     int rc = enqueue_sift_stereo(c, set, d_lefts, d_rights, B, sync);
     if (rc) return rc;
     c->last_B = B;
