@@ -59,11 +59,26 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (not used by the driver): several ranks on one GPU over gloo
+    if os.environ.get("VO_BENCH_SAME_GPU"):
+        local = 0
+    backend = os.environ.get("VO_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+
+    def max_over_ranks(x: float) -> float:
+        if dist is None:
+            return x
+        dev = f"cuda:{local}" if backend == "nccl" else "cpu"
+        t = torch.tensor([x], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
     B = args.batch
     # synthetic pairs: rank r renders frames [r*B, (r+1)*B) (seed 0x5EED0000 + frame)
@@ -90,10 +105,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
-    if dist is not None:
-        t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed)
     frames = B * args.steps * world
     fps = frames / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -178,10 +190,7 @@ def main():
         torch.cuda.synchronize()
         fel = time.perf_counter() - t0
         barrier()
-        if dist is not None:
-            t = torch.tensor([fel], device=f"cuda:{local}", dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            fel = float(t.item())
+        fel = max_over_ranks(fel)
         ok = outs["status"][1:] == 0
         full = {"metric": "stereo frames/sec, full per-frame path (BASELINE configs[2] on synthetic sequence)",
                 "value": nf * reps * world / fel, "unit": "stereo frames/s", "frames_per_rank": nf, "batch": B,
