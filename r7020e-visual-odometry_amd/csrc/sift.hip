@@ -526,7 +526,7 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
             const float* rowp_ = sp + (size_t)yin_ * pitch;                                       \
             if (!EDGE) {                                                                          \
                 pf[SL] = *reinterpret_cast<const vo_f4*>(rowp_ + xl);                             \
-                ph[SL] = *reinterpret_cast<const vo_f4*>(rowp_ + hx);                             \
+                if (!(TAG & 64)) ph[SL] = *reinterpret_cast<const vo_f4*>(rowp_ + hx);            \
             } else {                                                                              \
                 pf[SL] = vo_f4{rowp_[cm[0]], rowp_[cm[1]], rowp_[cm[2]], rowp_[cm[3]]};           \
                 ph[SL] = vo_f4{rowp_[ch[0]], rowp_[ch[1]], rowp_[ch[2]], rowp_[ch[3]]};           \
@@ -559,22 +559,25 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                                up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, ch[2]), up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, ch[3])};
                 }
             }
-            *reinterpret_cast<vo_f4*>(row + R4 + 4 * lane) = vm;
-            *reinterpret_cast<vo_f4*>(hpos >= 0 ? row + hpos : dummy) = vh;
+            if (!(TAG & 32)) {                            // TAG & 32: probe variant without LDS staging
+                *reinterpret_cast<vo_f4*>(row + R4 + 4 * lane) = vm;
+                *reinterpret_cast<vo_f4*>(hpos >= 0 ? row + hpos : dummy) = vh;
+            }
             __syncthreads();                              // one-wave block: orders the LDS rows only
             VO_BS_LOAD(kk + P, u);
             float w[4 * NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                const vo_f4 t = *reinterpret_cast<const vo_f4*>(row + 4 * lane + 4 * q);
+                const vo_f4 t = (TAG & 32) ? (q & 1 ? vh : vm) : *reinterpret_cast<const vo_f4*>(row + 4 * lane + 4 * q);
                 w[4 * q] = t.x; w[4 * q + 1] = t.y; w[4 * q + 2] = t.z; w[4 * q + 3] = t.w;
             }
             float h[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 float acc = k[0] * w[R4 + i];
+                if (!(TAG & 8))                           // TAG & 8: probe variant without the row pass
 #pragma unroll
-                for (int j = 1; j <= RAD; ++j) acc = fmaf(k[j], w[R4 + i - j] + w[R4 + i + j], acc);
+                    for (int j = 1; j <= RAD; ++j) acc = fmaf(k[j], w[R4 + i - j] + w[R4 + i + j], acc);
                 h[i] = acc;
             }
             H[2 * RAD + u][0] = vo_f2{h[0], h[1]};
@@ -584,9 +587,10 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
                     vo_f2 acc = vo_f2{k[0], k[0]} * H[u + RAD][c];
+                    if (!(TAG & 16))                      // TAG & 16: probe variant without the column pass
 #pragma unroll
-                    for (int j = 1; j <= RAD; ++j)
-                        acc = __builtin_elementwise_fma(vo_f2{k[j], k[j]}, H[u + RAD - j][c] + H[u + RAD + j][c], acc);
+                        for (int j = 1; j <= RAD; ++j)
+                            acc = __builtin_elementwise_fma(vo_f2{k[j], k[j]}, H[u + RAD - j][c] + H[u + RAD + j][c], acc);
                     o[c] = acc;
                 }
                 const vo_f4 g4 = vo_f4{o[0].x, o[0].y, o[1].x, o[1].y};
@@ -610,7 +614,9 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
 }
 
 // TAG: 0 level blur, 1 octave-0 base from a float plane, 5 octave-0 base with the x2
-// upsample of the u8 image fused (isrc), 2 cached-store variant (experiments)
+// upsample of the u8 image fused (isrc); instrumentation variants used only by
+// tools/blur_probe.hip: 2 cached stores, 8 no row pass, 16 no column pass,
+// 32 no LDS staging, 64 no halo loads
 template <int RAD, int TAG>
 __global__ __launch_bounds__(64, RAD <= 6 ? 3 : 2) void k_blur_stream(const float* __restrict__ src, size_t splane, size_t dplane,
                                                     int pitch, int R, int C, float* __restrict__ g_out, Kern K,
@@ -1540,7 +1546,7 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
     static const int use_pipe = getenv("VO_BLUR_PIPE") ? atoi(getenv("VO_BLUR_PIPE")) : 0;
     if constexpr (MODE == 0 && RAD > 0) if (!use_pipe) {
         static const int th_env = getenv("VO_BLUR_TH") ? atoi(getenv("VO_BLUR_TH")) : 48;
-        static const int wave_target = getenv("VO_BLUR_WAVES") ? atoi(getenv("VO_BLUR_WAVES")) : 2048;
+        static const int wave_target = getenv("VO_BLUR_WAVES") ? atoi(getenv("VO_BLUR_WAVES")) : 1024;
         // band height: a multiple of P, at most th_env, lowered on small octaves until
         // the launch has ~wave_target waves (8 per CU) -- small planes are latency-bound
         const int n_strips = (C + BS_W - 1) / BS_W;
