@@ -1,0 +1,228 @@
+"""KITTI odometry I/O, trajectory output, accuracy evaluation and map persistence
+(host side, around the libvo hot path).
+
+Mirrors what `VO.m` does around its per-frame loop:
+  * sequence layout and loading   -- `VO.m:13-17` (times.txt, image_0/image_1 PNG datastores),
+    `VO.m:23-38` (calib.txt: P0/P1 rows read with `readmatrix`, columns 2:13, row-major 3x4);
+  * undistortImage (`VO.m:75-76`) is the identity: `cameraIntrinsics` is built with zero
+    distortion (`VO.m:50-51`), so frames go to libvo unchanged (`undistort_identity` states it);
+  * trajectory                    -- `VO.m:130-134` (`pose = pose * rel_pose`, `all_poses`),
+    written in the KITTI 3x4 row-major pose format;
+  * accuracy                      -- `PlotOnMap.m:1-26`: the reference's lagged xz error
+    (estimate of frame k against ground truth of frame k-1, quirk Q5) and the plain
+    absolute trajectory error (ATE RMSE, frames aligned by index, both anchored at frame 0);
+  * landmark map                  -- `CreateLandmarksFromFeatures.m:20`, `VO.m:253`: the
+    accumulated world points as .npy and ASCII .ply.
+
+PNG decoding runs on host threads (PIL) ahead of the GPU; batches are staged in pinned host
+memory and copied to the device asynchronously.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+from dataclasses import dataclass
+from pathlib import Path
+
+import numpy as np
+
+
+# ---------------------------------------------------------------------------------------
+# text formats
+# ---------------------------------------------------------------------------------------
+def read_calib(path: str | os.PathLike) -> dict[str, np.ndarray]:
+    """calib.txt -> {"P0": 3x4, "P1": 3x4, ...}.  Same values as `VO.m:23-32`
+    (readmatrix drops the "Pk:" label column; columns 2:13 reshaped row-major)."""
+    out = {}
+    for line in Path(path).read_text().splitlines():
+        if ":" not in line:
+            continue
+        key, vals = line.split(":", 1)
+        v = np.array([float(x) for x in vals.split()], np.float64)
+        if v.size == 12:
+            out[key.strip()] = v.reshape(3, 4)
+    if "P0" not in out or "P1" not in out:
+        raise ValueError(f"{path}: no P0/P1 rows")
+    return out
+
+
+def read_times(path: str | os.PathLike) -> np.ndarray:
+    """times.txt -> seconds per frame (`VO.m:13`)."""
+    return np.array([float(x) for x in Path(path).read_text().split()], np.float64)
+
+
+def read_poses(path: str | os.PathLike) -> np.ndarray:
+    """KITTI pose file (12 floats per line, 3x4 row-major camera-to-world) -> [n, 4, 4]."""
+    rows = [np.array([float(x) for x in ln.split()], np.float64) for ln in Path(path).read_text().splitlines()
+            if ln.strip()]
+    P = np.zeros((len(rows), 4, 4))
+    for i, r in enumerate(rows):
+        if r.size != 12:
+            raise ValueError(f"{path}:{i + 1}: expected 12 values, got {r.size}")
+        P[i, :3, :] = r.reshape(3, 4)
+        P[i, 3, 3] = 1.0
+    return P
+
+
+def write_poses(path: str | os.PathLike, poses: np.ndarray) -> None:
+    """[n, 4, 4] camera-to-world poses -> KITTI pose file (frame 0 first)."""
+    with open(path, "w") as f:
+        for T in np.asarray(poses, np.float64):
+            f.write(" ".join(f"{v:.9e}" for v in T[:3, :].reshape(-1)) + "\n")
+
+
+# ---------------------------------------------------------------------------------------
+# accuracy (PlotOnMap.m)
+# ---------------------------------------------------------------------------------------
+def lagged_xz_error(est: np.ndarray, gt: np.ndarray) -> np.ndarray:
+    """The reference's error curve (`PlotOnMap.m:8-20`): for j = 1..n-1 (1-based all_poses
+    index), || xz(GT row j) - xz(all_poses(j)) || where all_poses(j) is the estimate of
+    0-based frame j and GT row j is 0-based frame j-1 -- a one-frame lag (quirk Q5).
+    `est` and `gt` are [n, 4, 4] with frame 0 first; returns n-1 errors."""
+    est = np.asarray(est, np.float64)
+    gt = np.asarray(gt, np.float64)
+    n = min(len(est), len(gt) + 1)
+    t_est = est[1:n, [0, 2], 3]
+    t_gt = gt[0:n - 1, [0, 2], 3]
+    return np.linalg.norm(t_gt - t_est, axis=1)
+
+
+def ate_rmse(est: np.ndarray, gt: np.ndarray) -> float:
+    """Absolute trajectory error: RMSE of camera positions, frames matched by index, both
+    trajectories anchored at frame 0 (KITTI GT frame 0 is the identity, as is ours)."""
+    est = np.asarray(est, np.float64)
+    gt = np.asarray(gt, np.float64)
+    n = min(len(est), len(gt))
+    d = est[:n, :3, 3] - gt[:n, :3, 3]
+    return float(np.sqrt(np.mean(np.sum(d * d, axis=1))))
+
+
+# ---------------------------------------------------------------------------------------
+# landmark map (CreateLandmarksFromFeatures.m:20, VO.m:253)
+# ---------------------------------------------------------------------------------------
+def save_landmarks(path: str | os.PathLike, pts: np.ndarray) -> None:
+    """Write the accumulated map: .npy (float64 [L, 3]) or ASCII .ply by extension.
+    Zero rows (quirk Q4) are kept, as the reference's `landmarks` array keeps them."""
+    pts = np.asarray(pts, np.float64).reshape(-1, 3)
+    p = Path(path)
+    if p.suffix == ".npy":
+        np.save(p, pts)
+    elif p.suffix == ".ply":
+        with open(p, "w") as f:
+            f.write("ply\nformat ascii 1.0\n")
+            f.write(f"element vertex {len(pts)}\nproperty double x\nproperty double y\nproperty double z\n")
+            f.write("end_header\n")
+            for x, y, z in pts:
+                f.write(f"{x:.9g} {y:.9g} {z:.9g}\n")
+    else:
+        raise ValueError(f"{path}: use .npy or .ply")
+
+
+def load_landmarks(path: str | os.PathLike) -> np.ndarray:
+    p = Path(path)
+    if p.suffix == ".npy":
+        return np.load(p)
+    lines = p.read_text().splitlines()
+    n = int(next(ln for ln in lines if ln.startswith("element vertex")).split()[2])
+    start = lines.index("end_header") + 1
+    return np.array([[float(v) for v in ln.split()] for ln in lines[start:start + n]], np.float64).reshape(-1, 3)
+
+
+# ---------------------------------------------------------------------------------------
+# sequence loading
+# ---------------------------------------------------------------------------------------
+def undistort_identity() -> bool:
+    """`VO.m:75-76` undistortImage with the zero-distortion intrinsics of `VO.m:50-51` is the
+    identity map (bilinear at integer sample positions, OutputView 'same'); frames are
+    passed through unchanged."""
+    return True
+
+
+def _read_png(path: Path) -> np.ndarray:
+    from PIL import Image
+    with Image.open(path) as im:
+        if im.mode != "L":
+            im = im.convert("L")
+        return np.asarray(im, np.uint8).copy()
+
+
+@dataclass
+class KittiSequence:
+    """A KITTI odometry sequence in the reference's layout:
+    <root>/<seq>/{image_0,image_1}/%06d.png, <root>/<seq>/{calib.txt,times.txt},
+    optional ground truth <root>/poses/<seq>.txt."""
+    root: Path
+    seq: str = "00"
+    threads: int = 8
+
+    def __post_init__(self):
+        self.root = Path(self.root)
+        d = self.root / self.seq
+        self.left = sorted((d / "image_0").glob("*.png"))
+        self.right = sorted((d / "image_1").glob("*.png"))
+        if not self.left or len(self.left) != len(self.right):
+            raise FileNotFoundError(f"{d}: image_0/image_1 PNG lists missing or of different length")
+        cal = read_calib(d / "calib.txt")
+        self.P1, self.P2 = cal["P0"], cal["P1"]          # VO.m's p1 / p2 (left, right)
+        self.times = read_times(d / "times.txt") if (d / "times.txt").exists() else None
+        gt = self.root / "poses" / f"{self.seq}.txt"
+        self.gt = read_poses(gt) if gt.exists() else None
+        first = _read_png(self.left[0])
+        self.rows, self.cols = first.shape
+        self._pool = cf.ThreadPoolExecutor(max_workers=self.threads)
+
+    def __len__(self) -> int:
+        return len(self.left)
+
+    def _load(self, i: int) -> tuple[np.ndarray, np.ndarray]:
+        l, r = _read_png(self.left[i]), _read_png(self.right[i])
+        if l.shape != (self.rows, self.cols) or r.shape != (self.rows, self.cols):
+            raise ValueError(f"frame {i}: image size differs from frame 0")
+        return l, r
+
+    def batches(self, batch: int, start: int = 0, stop: int | None = None):
+        """Yield (first_frame, L [b, H, W] u8, R [b, H, W] u8); PNG decode of the next batch
+        runs on the thread pool while the caller processes the current one."""
+        stop = len(self) if stop is None else min(stop, len(self))
+
+        def submit(b0):
+            return [self._pool.submit(self._load, i) for i in range(b0, min(b0 + batch, stop))]
+
+        pending = submit(start) if start < stop else None
+        b0 = start
+        while pending:
+            nxt = b0 + batch
+            ahead = submit(nxt) if nxt < stop else None
+            pairs = [f.result() for f in pending]
+            yield b0, np.stack([p[0] for p in pairs]), np.stack([p[1] for p in pairs])
+            pending, b0 = ahead, nxt
+
+    def close(self):
+        self._pool.shutdown(wait=True)
+
+
+def run(seq: KittiSequence, batch: int = 16, stop: int | None = None, device: int = 0, ctx=None):
+    """The VO.m loop over a KITTI sequence through libvo: frames in batches of `batch`
+    (vo_step_batch_dev, tracking carried across batches), H2D from pinned host buffers.
+    Returns (poses [n, 4, 4] with frame 0 = identity, per-frame vo_step_out records,
+    landmarks [L, 3])."""
+    import torch
+    from . import vo
+    own = ctx is None
+    if own:
+        ctx = vo.Context(seq.rows, seq.cols, batch, device=device, calib=vo.calib_from(seq.P1, seq.P2))
+    outs = []
+    dev = torch.device("cuda", device)
+    for _b0, L, R in seq.batches(batch, 0, stop):
+        hl = torch.from_numpy(L).pin_memory()
+        hr = torch.from_numpy(R).pin_memory()
+        dl = hl.to(dev, non_blocking=True)
+        dr = hr.to(dev, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        outs.append(ctx.step_batch_dev(dl.data_ptr(), dr.data_ptr(), L.shape[0]))
+    outs = np.concatenate(outs) if outs else np.zeros(0, vo.STEP_DTYPE)
+    poses = np.stack([o["pose"] for o in outs]) if len(outs) else np.zeros((0, 4, 4))
+    lm = ctx.get_landmarks()
+    if own:
+        ctx.close()
+    return poses, outs, lm
