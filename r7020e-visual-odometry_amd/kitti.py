@@ -226,3 +226,46 @@ def run(seq: KittiSequence, batch: int = 16, stop: int | None = None, device: in
     if own:
         ctx.close()
     return poses, outs, lm
+
+
+def run_shard(seq: KittiSequence, rank: int, world: int, batch: int = 16, device: int = 0,
+              stop: int | None = None) -> np.ndarray:
+    """One rank's part of a frame-sharded run (`sharding.py`): the block
+    [start, end) of frames plus a one-frame halo, MSAC keyed by the global frame index.
+    Returns the block's relative poses [end - start, 4, 4] (frame 0's is the identity)."""
+    import torch
+    from . import sharding, vo
+    n = len(seq) if stop is None else min(stop, len(seq))
+    s, e = sharding.shard_range(n, world, rank)
+    h = sharding.halo_start(s)
+    ctx = vo.Context(seq.rows, seq.cols, batch, device=device, calib=vo.calib_from(seq.P1, seq.P2))
+    ctx.reset()
+    ctx.set_frame_index(h)
+    dev = torch.device("cuda", device)
+    outs = []
+    for _b0, L, R in seq.batches(batch, h, e):
+        dl = torch.from_numpy(L).pin_memory().to(dev, non_blocking=True)
+        dr = torch.from_numpy(R).pin_memory().to(dev, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        outs.append(ctx.step_batch_dev(dl.data_ptr(), dr.data_ptr(), L.shape[0]))
+    ctx.close()
+    outs = np.concatenate(outs)
+    return outs["rel_pose"][s - h:]
+
+
+def run_distributed(seq: KittiSequence, batch: int = 16, device: int = 0, stop: int | None = None,
+                    group=None) -> np.ndarray:
+    """Frame-sharded run over a torch.distributed group (one process per GPU; RCCL over
+    xGMI with the nccl backend): every rank runs its block (`run_shard`), one all-gather
+    of 16 doubles per frame collects the relative poses, and the world-pose chain is the
+    host product of `VO.m:130`.  Returns world poses [n, 4, 4] on every rank, equal bit for
+    bit to a single-process run.  (The landmark map needs the world chain before its
+    transform step; use `run` for it.)"""
+    import torch
+    import torch.distributed as dist
+    from . import sharding
+    n = len(seq) if stop is None else min(stop, len(seq))
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    rel = run_shard(seq, rank, world, batch, device, n)
+    dev = torch.device("cuda", device) if dist.get_backend(group) == "nccl" else None
+    return sharding.chain(sharding.gather_rel_poses(rel, n, group=group, device=dev))

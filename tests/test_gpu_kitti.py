@@ -29,3 +29,22 @@ def test_kitti_driver_matches_host_stepping(vo, syn, tmp_path):
     assert np.allclose(kitti.read_poses(tmp_path / "est.txt"), poses, rtol=1e-9, atol=1e-12)
     kitti.save_landmarks(tmp_path / "map.ply", lm)
     assert kitti.load_landmarks(tmp_path / "map.ply").shape == lm.shape
+
+
+def test_sharded_blocks_chain_to_single_run(vo, syn, tmp_path):
+    """Frame sharding (block + one-frame halo, MSAC keyed by the global frame index):
+    the ranks' relative poses, chained on the host, equal the single-process world poses
+    bit for bit (ranks simulated one after another on the one GPU of this box)."""
+    import vo_amd  # noqa: F401
+    from r7020e_visual_odometry_amd import kitti, sharding
+    from test_kitti import write_kitti_layout
+    n = 9
+    L, R, _gt = syn.sequence(n, step_m=0.5)
+    write_kitti_layout(tmp_path, L, R)
+    seq = kitti.KittiSequence(tmp_path, "00")
+    poses, outs, _lm = kitti.run(seq, batch=3)
+    for world in (2, 3):
+        rel = np.concatenate([kitti.run_shard(seq, r, world, batch=3) for r in range(world)])
+        assert rel.shape == (n, 4, 4)
+        assert np.array_equal(sharding.chain(rel), poses), world
+    seq.close()
