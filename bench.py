@@ -154,6 +154,8 @@ def main():
     pyr_bytes = 2 * B * roofline.pyramid_bytes_per_image(ROWS, COLS)
     roof["pyramid_model_gbs"] = pyr_bytes / (pyr_ms * 1e-3) / 1e9 if pyr_ms > 0 else None
     roof["kernel_ms_per_step"] = {n: round(v[0] / args.profile_steps, 4) for n, v in sorted(kt.items(), key=lambda kv: -kv[1][0])}
+    roof["kernel_ms_per_step_isolated"] = {n: round(v[0] / args.profile_steps, 4)
+                                           for n, v in sorted(kt_iso.items(), key=lambda kv: -kv[1][0])}
 
     # ---- BASELINE configs[2] on synthetic data: the full per-frame path (SIFT x2, stereo
     # match, tracking matches, DLT, P3P+MSAC 2048 hypotheses, landmarks) over a moving-camera
