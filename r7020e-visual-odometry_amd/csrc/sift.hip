@@ -442,10 +442,10 @@ __device__ inline int xcd_remap(int bid, int n)
     return xcd < rm ? xcd * (q + 1) + idx : rm * (q + 1) + (xcd - rm) * q + idx;
 }
 
-#define BS_W 256          // strip width (64 lanes x 4 columns)
 #define BS_P 4            // prefetch depth (rows)
-__host__ __device__ constexpr int bs_r4(int r) { return (r + 3) & ~3; }
-__host__ __device__ constexpr int bs_rw(int r) { return BS_W + 2 * bs_r4(r); }
+// halo floats each side, rounded up to whole CPL-column vectors; staged row length
+__host__ __device__ constexpr int bs_rh(int r, int cpl) { return (r + cpl - 1) / cpl * cpl; }
+__host__ __device__ constexpr int bs_rw(int r, int cpl) { return 64 * cpl + 2 * bs_rh(r, cpl); }
 
 // u8 source of the octave-0 base level (TAG & 4): the x2 upsample is formed
 // while staging each input row, from raw source words prefetched like floats.
@@ -466,32 +466,38 @@ __device__ __forceinline__ vo_f4 up4_from_words(uint32_t a0, uint32_t a1, uint32
     return vo_f4{r[0], r[1], r[2], r[3]};
 }
 
-template <int RAD, bool EDGE, int TAG>
+template <int RAD, bool EDGE, int TAG, int CPL>
 __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, int pitch, int R, int C,
                                                  float* __restrict__ g_out, const Kern& K,
                                                  int x0, int y0, int TH, float* rb, const U8Src& u8)
 {
+    // CPL columns per lane (4: 256-column strips, 16-B accesses; 2: 128-column strips,
+    // 8-B accesses, half the ring registers -> more waves for the smaller octaves)
+    typedef float vec_t __attribute__((ext_vector_type(CPL)));
     constexpr bool UP = (TAG & 4) != 0;
+    static_assert(!UP || CPL == 4, "the fused x2 upsample uses 4 columns per lane");
+    constexpr int SW = 64 * CPL;                           // strip width
     constexpr int P = BS_P;                                // prefetch depth = steps per loop block
-    constexpr int R4 = bs_r4(RAD);                         // halo rounded to whole float4s
-    constexpr int NQ = 1 + R4 / 2;                         // float4 reads per lane window
+    constexpr int RH = bs_rh(RAD, CPL);                    // halo rounded to whole vectors
+    constexpr int NQ = 1 + 2 * RH / CPL;                   // vector reads per lane window
+    constexpr int NP = CPL / 2;                            // float2 column pairs per lane
     constexpr int NR = 2 * RAD + P;                        // ring: 2r carried rows + P new per block
     constexpr int F = (2 * RAD + P - 1) / P * P;           // ring-fill steps (no output)
     constexpr int E = F - 2 * RAD;                         // extra rows read above the band
-    constexpr int RW = bs_rw(RAD);                         // staged row floats (one LDS ring slot)
+    constexpr int RW = bs_rw(RAD, CPL);                    // staged row floats
     const int lane = threadIdx.x;
-    const int xl = x0 + 4 * lane;
-    // halo lanes: [0, R4/4) left, [R4/4, R4/2) right.  The others load lane 0's
-    // segment (same cache line) and stage it into a private dummy LDS slot, so
-    // every lane issues the same instructions.
-    const bool hl = lane < R4 / 4, hr = !hl && lane < R4 / 2;
-    const int hx = hl ? x0 - R4 + 4 * lane : hr ? x0 + BS_W + 4 * (lane - R4 / 4) : x0 - R4;
-    const int hpos = hl ? 4 * lane : hr ? R4 + BS_W + 4 * (lane - R4 / 4) : -1;
-    float* const dummy = rb + RW + 4 * lane;
-    int cm[4], ch[4];                                      // border strips: reflect-101 source columns
+    const int xl = x0 + CPL * lane;
+    // halo lanes: [0, RH/CPL) left, [RH/CPL, 2*RH/CPL) right.  The others load lane 0's
+    // segment (same cache line) and stage it into a private dummy LDS slot, so every
+    // lane issues the same instructions.
+    const bool hl = lane < RH / CPL, hr = !hl && lane < 2 * RH / CPL;
+    const int hx = hl ? x0 - RH + CPL * lane : hr ? x0 + SW + CPL * (lane - RH / CPL) : x0 - RH;
+    const int hpos = hl ? CPL * lane : hr ? RH + SW + CPL * (lane - RH / CPL) : -1;
+    float* const dummy = rb + RW + CPL * lane;
+    int cm[CPL], ch[CPL];                                  // border strips: reflect-101 source columns
     if (EDGE) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < CPL; ++i) {
             cm[i] = vo_reflect101(xl + i, C);
             ch[i] = vo_reflect101(hx + i, C);
         }
@@ -500,19 +506,26 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
 #pragma unroll
     for (int j = 0; j <= RAD; ++j) k[j] = K.k[j];
 
-    vo_f4 pf[P], ph[P];
+    vec_t pf[P], ph[P];
     typedef uint32_t u2_t __attribute__((ext_vector_type(2)));
     u2_t pw[UP && !EDGE ? P : 1][4];                       // UP: raw words (ya main, yb main, ya halo, yb halo)
-    vo_f2 H[NR][2];
+    vo_f2 H[NR][NP];
     // UP: source byte column of the first of the 4 bytes feeding outputs xl.. / hx..
     const int gm = (xl >> 1) - 1, gh = (hx >> 1) - 1;
+
+    auto gather = [&](const float* rowp, const int* idx) {
+        vec_t v;
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) v[i] = rowp[idx[i]];
+        return v;
+    };
 
     // loads for step kk into prefetch slot SL: input row y0-r-E+kk (reflected)
 #define VO_BS_LOAD(KK, SL)                                                                        \
     do {                                                                                          \
         const int yin_ = vo_reflect101(y0 - RAD - E + (KK), R);                                   \
-        if (UP) {                                                                                 \
-            if (!EDGE) {                                                                          \
+        if constexpr (UP) {                                                                       \
+            if constexpr (!EDGE) {                                                                \
                 const int ya_ = yin_ >> 1;                                                        \
                 const int yb_ = (yin_ & 1) ? min(ya_ + 1, u8.rows - 1) : max(ya_ - 1, 0);         \
                 const uint8_t* ra_ = u8.p + (size_t)ya_ * u8.ld;                                  \
@@ -524,12 +537,12 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
             }                                                                                     \
         } else {                                                                                  \
             const float* rowp_ = sp + (size_t)yin_ * pitch;                                       \
-            if (!EDGE) {                                                                          \
-                pf[SL] = *reinterpret_cast<const vo_f4*>(rowp_ + xl);                             \
-                if (!(TAG & 64)) ph[SL] = *reinterpret_cast<const vo_f4*>(rowp_ + hx);            \
+            if constexpr (!EDGE) {                                                                \
+                pf[SL] = *reinterpret_cast<const vec_t*>(rowp_ + xl);                             \
+                if (!(TAG & 64)) ph[SL] = *reinterpret_cast<const vec_t*>(rowp_ + hx);            \
             } else {                                                                              \
-                pf[SL] = vo_f4{rowp_[cm[0]], rowp_[cm[1]], rowp_[cm[2]], rowp_[cm[3]]};           \
-                ph[SL] = vo_f4{rowp_[ch[0]], rowp_[ch[1]], rowp_[ch[2]], rowp_[ch[3]]};           \
+                pf[SL] = gather(rowp_, cm);                                                       \
+                ph[SL] = gather(rowp_, ch);                                                       \
             }                                                                                     \
         }                                                                                         \
     } while (0)
@@ -542,7 +555,7 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
             constexpr int u = decltype(uc)::value;
             const int kk = kk0 + u;
             float* const row = rb;
-            vo_f4 vm = pf[u], vh = ph[u];
+            vec_t vm = pf[u], vh = ph[u];
             if constexpr (UP) {
                 const int yin = vo_reflect101(y0 - RAD - E + kk, R);
                 if constexpr (!EDGE) {
@@ -553,56 +566,60 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                     vm = up4_from_words(pw[u][0].x, pw[u][0].y, sa, pw[u][1].x, pw[u][1].y, sb);
                     vh = up4_from_words(pw[u][2].x, pw[u][2].y, ha, pw[u][3].x, pw[u][3].y, hb);
                 } else {                                  // border strips: reflected columns, loads in place
-                    vm = vo_f4{up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, cm[0]), up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, cm[1]),
-                               up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, cm[2]), up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, cm[3])};
-                    vh = vo_f4{up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, ch[0]), up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, ch[1]),
-                               up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, ch[2]), up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, ch[3])};
+#pragma unroll
+                    for (int i = 0; i < CPL; ++i) {
+                        vm[i] = up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, cm[i]);
+                        vh[i] = up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, ch[i]);
+                    }
                 }
             }
             if (!(TAG & 32)) {                            // TAG & 32: probe variant without LDS staging
-                *reinterpret_cast<vo_f4*>(row + R4 + 4 * lane) = vm;
-                *reinterpret_cast<vo_f4*>(hpos >= 0 ? row + hpos : dummy) = vh;
+                *reinterpret_cast<vec_t*>(row + RH + CPL * lane) = vm;
+                *reinterpret_cast<vec_t*>(hpos >= 0 ? row + hpos : dummy) = vh;
             }
-            __syncthreads();                              // one-wave block: orders the LDS rows only
+            __syncthreads();                              // one-wave block: orders the LDS row only
             VO_BS_LOAD(kk + P, u);
-            float w[4 * NQ];
+            float w[CPL * NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                const vo_f4 t = (TAG & 32) ? (q & 1 ? vh : vm) : *reinterpret_cast<const vo_f4*>(row + 4 * lane + 4 * q);
-                w[4 * q] = t.x; w[4 * q + 1] = t.y; w[4 * q + 2] = t.z; w[4 * q + 3] = t.w;
-            }
-            float h[4];
+                const vec_t t = (TAG & 32) ? (q & 1 ? vh : vm) : *reinterpret_cast<const vec_t*>(row + CPL * lane + CPL * q);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float acc = k[0] * w[R4 + i];
+                for (int i = 0; i < CPL; ++i) w[CPL * q + i] = t[i];
+            }
+            float h[CPL];
+#pragma unroll
+            for (int i = 0; i < CPL; ++i) {
+                float acc = k[0] * w[RH + i];
                 if (!(TAG & 8))                           // TAG & 8: probe variant without the row pass
 #pragma unroll
-                    for (int j = 1; j <= RAD; ++j) acc = fmaf(k[j], w[R4 + i - j] + w[R4 + i + j], acc);
+                    for (int j = 1; j <= RAD; ++j) acc = fmaf(k[j], w[RH + i - j] + w[RH + i + j], acc);
                 h[i] = acc;
             }
-            H[2 * RAD + u][0] = vo_f2{h[0], h[1]};
-            H[2 * RAD + u][1] = vo_f2{h[2], h[3]};
-            if constexpr (decltype(store_c)::value) {
-                vo_f2 o[2];
 #pragma unroll
-                for (int c = 0; c < 2; ++c) {
+            for (int c = 0; c < NP; ++c) H[2 * RAD + u][c] = vo_f2{h[2 * c], h[2 * c + 1]};
+            if constexpr (decltype(store_c)::value) {
+                vec_t g;
+#pragma unroll
+                for (int c = 0; c < NP; ++c) {
                     vo_f2 acc = vo_f2{k[0], k[0]} * H[u + RAD][c];
                     if (!(TAG & 16))                      // TAG & 16: probe variant without the column pass
 #pragma unroll
                         for (int j = 1; j <= RAD; ++j)
                             acc = __builtin_elementwise_fma(vo_f2{k[j], k[j]}, H[u + RAD - j][c] + H[u + RAD + j][c], acc);
-                    o[c] = acc;
+                    g[2 * c] = acc.x;
+                    g[2 * c + 1] = acc.y;
                 }
-                const vo_f4 g4 = vo_f4{o[0].x, o[0].y, o[1].x, o[1].y};
                 // columns >= C land in the row padding (pitch is a whole number of strips)
                 const size_t off = (size_t)(y0 + kk - F) * pitch + xl;
-                if (TAG & 2) *reinterpret_cast<vo_f4*>(g_out + off) = g4;            // cached store variant
-                else __builtin_nontemporal_store(g4, reinterpret_cast<vo_f4*>(g_out + off));
+                if (TAG & 2) *reinterpret_cast<vec_t*>(g_out + off) = g;            // cached store variant
+                else __builtin_nontemporal_store(g, reinterpret_cast<vec_t*>(g_out + off));
             }
             __syncthreads();
         });
 #pragma unroll
-        for (int q = 0; q < 2 * RAD; ++q) { H[q][0] = H[q + P][0]; H[q][1] = H[q + P][1]; }
+        for (int q = 0; q < 2 * RAD; ++q)
+#pragma unroll
+            for (int c = 0; c < NP; ++c) H[q][c] = H[q + P][c];
     };
 
     vo_static_for<P>([&](auto uc) { VO_BS_LOAD(decltype(uc)::value, decltype(uc)::value); });
@@ -616,18 +633,18 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
 // TAG: 0 level blur, 1 octave-0 base from a float plane, 5 octave-0 base with the x2
 // upsample of the u8 image fused (isrc); instrumentation variants used only by
 // tools/blur_probe.hip: 2 cached stores, 8 no row pass, 16 no column pass,
-// 32 no LDS staging, 64 no halo loads
-template <int RAD, int TAG>
-__global__ __launch_bounds__(64, RAD <= 6 ? 3 : 2) void k_blur_stream(const float* __restrict__ src, size_t splane, size_t dplane,
-                                                    int pitch, int R, int C, float* __restrict__ g_out, Kern K,
-                                                    int n_strips, int n_bands, int TH, ImageSrc isrc, int in_rows, int in_cols)
+// 32 no LDS staging, 64 no halo loads.  CPL: columns per lane (4 or 2).
+template <int RAD, int TAG, int CPL = 4>
+__global__ __launch_bounds__(64, (RAD <= 6 || CPL == 2) ? 3 : 2) void k_blur_stream(
+    const float* __restrict__ src, size_t splane, size_t dplane, int pitch, int R, int C, float* __restrict__ g_out, Kern K,
+    int n_strips, int n_bands, int TH, ImageSrc isrc, int in_rows, int in_cols)
 {
-    constexpr int R4 = bs_r4(RAD);
-    __shared__ __attribute__((aligned(16))) float rb[bs_rw(RAD) + 256];   // staged row + per-lane dummy halo slots
+    constexpr int RH = bs_rh(RAD, CPL), SW = 64 * CPL;
+    __shared__ __attribute__((aligned(16))) float rb[bs_rw(RAD, CPL) + 64 * CPL];   // staged row + per-lane dummy halo slots
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int strip = bid % n_strips, tb = bid / n_strips;
     const int band = tb % n_bands, img = tb / n_bands;
-    const int x0 = strip * BS_W, y0 = min(band * TH, R - TH);
+    const int x0 = strip * SW, y0 = min(band * TH, R - TH);
     const size_t os = img * splane, od = img * dplane;
     U8Src u8{nullptr, 0, in_rows, in_cols};
     int margin = 0;
@@ -636,10 +653,10 @@ __global__ __launch_bounds__(64, RAD <= 6 ? 3 : 2) void k_blur_stream(const floa
         u8.ld = isrc.ld;
         margin = 16;                                       // 8-B word loads stay inside the source row
     }
-    if (x0 - R4 < 0 || x0 + BS_W + R4 + margin > C)
-        blur_stream_body<RAD, true, TAG>(src + os, pitch, R, C, g_out + od, K, x0, y0, TH, rb, u8);
+    if (x0 - RH < 0 || x0 + SW + RH + margin > C)
+        blur_stream_body<RAD, true, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, TH, rb, u8);
     else
-        blur_stream_body<RAD, false, TAG>(src + os, pitch, R, C, g_out + od, K, x0, y0, TH, rb, u8);
+        blur_stream_body<RAD, false, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, TH, rb, u8);
 }
 
 // next octave base.  grid over outputs
@@ -1549,7 +1566,13 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
         static const int wave_target = getenv("VO_BLUR_WAVES") ? atoi(getenv("VO_BLUR_WAVES")) : 1024;
         // band height: a multiple of P, at most th_env, lowered on small octaves until
         // the launch has ~wave_target waves (8 per CU) -- small planes are latency-bound
-        const int n_strips = (C + BS_W - 1) / BS_W;
+        // level blurs of planes at most cpl2_maxc wide use 2 columns per lane (128-column
+        // strips, half the ring registers): more waves and fewer idle lanes at the
+        // narrow octaves, where the kernel is latency-bound rather than HBM-bound
+        static const int cpl2_maxc = getenv("VO_BLUR_CPL2_MAXC") ? atoi(getenv("VO_BLUR_CPL2_MAXC")) : 1400;
+        const bool base = name[7] == 'b';
+        const int cpl = (!base && C <= cpl2_maxc) ? 2 : 4;
+        const int n_strips = (C + 64 * cpl - 1) / (64 * cpl);
         const long rows_total = (long)R * n_strips * grid.z;
         int TH = (int)std::min<long>(th_env, rows_total / wave_target);
         TH = std::max(BS_P, TH / BS_P * BS_P);
@@ -1557,18 +1580,15 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
             const int n_bands = (R + TH - 1) / TH;
             const int blocks = n_strips * n_bands * (int)grid.z;
             static const int cached = getenv("VO_BLUR_CACHED") ? atoi(getenv("VO_BLUR_CACHED")) : 0;
-            if (name[7] == 'b' && src == nullptr)      // "k_blur_base" from the u8 image (x2 upsample fused)
-                VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, 5>), dim3(blocks), dim3(64), 0, s, src, plane, dplane, pitch, R,
-                                C, g, K, n_strips, n_bands, TH, isrc, in_rows, in_cols);
-            else if (name[7] == 'b')
-                VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, 1>), dim3(blocks), dim3(64), 0, s, src, plane, dplane, pitch, R,
-                                C, g, K, n_strips, n_bands, TH, isrc, in_rows, in_cols);
-            else if (cached)
-                VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, 2>), dim3(blocks), dim3(64), 0, s, src, plane, dplane, pitch, R,
-                                C, g, K, n_strips, n_bands, TH, isrc, in_rows, in_cols);
-            else
-                VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, 0>), dim3(blocks), dim3(64), 0, s, src, plane, dplane, pitch, R,
-                                C, g, K, n_strips, n_bands, TH, isrc, in_rows, in_cols);
+#define VO_BS_GO(T, CP)                                                                                               \
+    VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, T, CP>), dim3(blocks), dim3(64), 0, s, src, plane, dplane, pitch, R, C, g, \
+                    K, n_strips, n_bands, TH, isrc, in_rows, in_cols)
+            if (base && src == nullptr) VO_BS_GO(5, 4);      // "k_blur_base" from the u8 image (x2 upsample fused)
+            else if (base) VO_BS_GO(1, 4);
+            else if (cpl == 2) { if (cached) VO_BS_GO(2, 2); else VO_BS_GO(0, 2); }
+            else if (cached) VO_BS_GO(2, 4);
+            else VO_BS_GO(0, 4);
+#undef VO_BS_GO
             return;
         }
     }

@@ -46,21 +46,21 @@ __global__ __launch_bounds__(64) void k_copy_strip(const float* __restrict__ a, 
     }
 }
 
-template <int RAD, int TAG>
+template <int RAD, int TAG, int CPL = 4>
 static float run(const float* src, float* dst, size_t plane, int pitch, int R, int C, int n_img, int TH, const Kern& K)
 {
-    const int n_strips = (C + BS_W - 1) / BS_W, n_bands = (R + TH - 1) / TH;
+    const int n_strips = (C + 64 * CPL - 1) / (64 * CPL), n_bands = (R + TH - 1) / TH;
     const int blocks = n_strips * n_bands * n_img;
     ImageSrc isrc{};
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
     for (int w = 0; w < 2; ++w)
-        hipLaunchKernelGGL((k_blur_stream<RAD, TAG>), dim3(blocks), dim3(64), 0, 0, src, plane, plane, pitch, R, C, dst, K,
+        hipLaunchKernelGGL((k_blur_stream<RAD, TAG, CPL>), dim3(blocks), dim3(64), 0, 0, src, plane, plane, pitch, R, C, dst, K,
                            n_strips, n_bands, TH, isrc, 0, 0);
     hipEventRecord(a);
     const int it = 10;
     for (int i = 0; i < it; ++i)
-        hipLaunchKernelGGL((k_blur_stream<RAD, TAG>), dim3(blocks), dim3(64), 0, 0, src, plane, plane, pitch, R, C, dst, K,
+        hipLaunchKernelGGL((k_blur_stream<RAD, TAG, CPL>), dim3(blocks), dim3(64), 0, 0, src, plane, plane, pitch, R, C, dst, K,
                            n_strips, n_bands, TH, isrc, 0, 0);
     hipEventRecord(b);
     hipEventSynchronize(b);
@@ -84,8 +84,12 @@ static void probe(const float* src, float* dst, size_t plane, int pitch, int R, 
     float t2 = run<RAD, 2>(src, dst, plane, pitch, R, C, n, TH, K);
     float t56 = run<RAD, 56>(src, dst, plane, pitch, R, C, n, TH, K);
     float t120 = run<RAD, 120>(src, dst, plane, pitch, R, C, n, TH, K);
+    float c0 = run<RAD, 0, 2>(src, dst, plane, pitch, R, C, n, TH, K);
+    float c24 = run<RAD, 24, 2>(src, dst, plane, pitch, R, C, n, TH, K);
+    float c56 = run<RAD, 56, 2>(src, dst, plane, pitch, R, C, n, TH, K);
     printf("r=%2d  full %6.1f us (%5.0f GB/s) | no-row %6.1f | no-col %6.1f | neither %6.1f | cached %6.1f | "
            "no compute+no LDS %6.1f | +no halo %6.1f\n", RAD, t0, mb / t0 * 1e3, t8, t16, t24, t2, t56, t120);
+    printf("      CPL=2 full %6.1f us (%5.0f GB/s) | neither %6.1f | no compute+no LDS %6.1f\n", c0, mb / c0 * 1e3, c24, c56);
 }
 
 static void copy_ref(const float* src, float* dst, size_t plane, int pitch, int R, int C, int n)
@@ -108,14 +112,15 @@ static void copy_ref(const float* src, float* dst, size_t plane, int pitch, int 
 
 int main()
 {
-    const int R = 750, C = 2484, n = 64;
-    const int pitch = getenv("PITCH") ? atoi(getenv("PITCH")) : 2560;
+    const int R = getenv("ROWS") ? atoi(getenv("ROWS")) : 750, C = getenv("COLS") ? atoi(getenv("COLS")) : 2484, n = 64;
+    const int pitch = getenv("PITCH") ? atoi(getenv("PITCH")) : (C + 255) / 256 * 256;
     printf("pitch %d\n", pitch);
     const size_t plane = (size_t)R * pitch;
     float *src, *dst;
     hipMalloc(&src, sizeof(float) * plane * n);
     hipMalloc(&dst, sizeof(float) * plane * n);
     hipMemset(src, 0, sizeof(float) * plane * n);
+    printf("%d x %d, %d images\n", R, C, n);
     copy_ref(src, dst, plane, pitch, R, C, n);
     probe<5>(src, dst, plane, pitch, R, C, n);
     probe<8>(src, dst, plane, pitch, R, C, n);
