@@ -12,7 +12,9 @@ Prints ONE JSON line (rank 0) with the driver's contract fields plus
 `roofline` (dominant kernel, HIP-event durations measured in this process)
 and `cpu_baseline` (the CPU oracle on a bounded sample, rank 0 at N=1).
 `full_path` additionally times the full per-frame path (vo_step_batch_dev) over
-a synthetic moving-camera sequence (--full-frames, default 64; 0 skips).
+a synthetic moving-camera sequence (--full-frames, default 64; 0 skips), and
+`large` the 1920x1080 / ~8k keypoint configuration (configs[4]) per GPU with the
+i8-MFMA rate of its dense stereo match block (--large-batch, default 8; 0 skips).
 """
 from __future__ import annotations
 
@@ -31,6 +33,7 @@ import numpy as np  # noqa: E402
 
 ROWS, COLS = 375, 1242
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+I8_MFMA_PEAK_TOPS = 5000.0     # MI355X_MICROARCH.md "Matrix cores": I8 = 2x the dense BF16 ~2.5 PF per clock
 # per-launch HBM bytes of each kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes on this
 # workload (tools/pmc_passes.sh + tools/pmc_traffic.py; FETCH_SIZE doubled on gfx950)
 TRAFFIC_FILE = ROOT / "profiles" / "r01_pmc_traffic.json"
@@ -47,6 +50,8 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=3)
     ap.add_argument("--full-frames", type=int, default=64,
                     help="frames of the synthetic sequence timed through the full per-frame path (0: skip)")
+    ap.add_argument("--large-batch", type=int, default=8,
+                    help="1920x1080 (~8k keypoints) stereo pairs per step for the configs[4] figure (0: skip)")
     return ap.parse_args()
 
 
@@ -203,6 +208,50 @@ def main():
         fctx.close()
         del d_sl, d_sr
 
+    # ---- BASELINE configs[4]: 1920x1080 synthetic stereo, ~8k keypoints per image, the dense
+    # 8k x 8k descriptor block on the i8 matrix cores (k_match_partial) ----
+    large = None
+    if args.large_batch > 0:
+        LB = args.large_batch
+        GL, GR = syn.large_pairs(LB, first=rank * LB)
+        d_gl = torch.from_numpy(GL).to(f"cuda:{local}")
+        d_gr = torch.from_numpy(GR).to(f"cuda:{local}")
+        lctx = vo.Context(syn.LARGE_ROWS, syn.LARGE_COLS, LB, device=local)
+        lst = lctx.sift_match_batch_dev(d_gl.data_ptr(), d_gr.data_ptr(), LB, stats=True)
+        for _ in range(2):
+            lctx.sift_match_batch_dev(d_gl.data_ptr(), d_gr.data_ptr(), LB, stats=False)
+        lsteps = max(3, args.steps // 2)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(lsteps):
+            lctx.sift_match_batch_dev(d_gl.data_ptr(), d_gr.data_ptr(), LB, stats=False)
+        torch.cuda.synchronize()
+        lel = time.perf_counter() - t0
+        barrier()
+        lel = max_over_ranks(lel)
+        lctx.set_profiling(True)
+        for _ in range(args.profile_steps):
+            lctx.sift_match_batch_dev(d_gl.data_ptr(), d_gr.data_ptr(), LB, stats=True)
+        torch.cuda.synchronize()
+        lkt = lctx.kernel_times()
+        lctx.set_profiling(False)
+        # exact int8 MAC work of the stereo blocks: 2 ops x n1 x n2 x 128 per frame
+        ops = sum(2.0 * s_[0] * s_[1] * 128 for s_ in lst)
+        mp_ms = lkt.get("k_match_partial", (0.0, 1))[0] / args.profile_steps
+        large = {"metric": "stereo frames/sec @1920x1080 (SIFT x2 + stereo matchFeatures, BASELINE configs[4] per GPU)",
+                 "value": LB * lsteps * world / lel, "unit": "stereo frames/s", "batch": LB,
+                 "mean_keypoints_per_image": float(np.mean([s_[0] + s_[1] for s_ in lst]) / 2),
+                 "mean_stereo_matches": float(np.mean([s_[2] for s_ in lst])),
+                 "match_block": {"kernel": "k_match_partial", "bound": "mfma", "unit": "TOP/s (i8)",
+                                 "ops_per_step": ops, "ms_per_step": mp_ms,
+                                 "achieved": ops / (mp_ms * 1e-3) / 1e12 if mp_ms > 0 else None,
+                                 "peak": I8_MFMA_PEAK_TOPS,
+                                 "frac": ops / (mp_ms * 1e-3) / 1e12 / I8_MFMA_PEAK_TOPS if mp_ms > 0 else None},
+                 "kernel_ms_per_step": {n: round(v[0] / args.profile_steps, 4)
+                                        for n, v in sorted(lkt.items(), key=lambda kv: -kv[1][0])}}
+        lctx.close()
+        del d_gl, d_gr
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         import oracle
@@ -231,6 +280,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "full_path": full,
+            "large": large,
         }
         print(json.dumps(line))
     if dist is not None:

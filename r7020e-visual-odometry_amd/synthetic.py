@@ -31,6 +31,9 @@ KITTI00_P1 = np.array([[718.856, 0.0, 607.1928, -386.1448],
                        [0.0, 718.856, 185.2157, 0.0],
                        [0.0, 0.0, 1.0, 0.0]])
 SEED_BASE = 0x5EED0000
+# BASELINE configs[4]: 1920x1080, ~8k keypoints per image.  At the default 16 px per texture
+# cell the oracle finds ~6.8k; 14.5 px per cell gives 8k +- 10 % (tests/test_gpu_large.py).
+LARGE_ROWS, LARGE_COLS, LARGE_PX_PER_CELL = 1080, 1920, 14.5
 
 
 @dataclass
@@ -152,13 +155,20 @@ def stereo_pair(seed: int, rows: int = 375, cols: int = 1242, noise_sd: float = 
     return _to_u8(left, rng, noise_sd), _to_u8(right, rng, noise_sd)
 
 
-def independent_pairs(n: int, rows: int = 375, cols: int = 1242, first: int = 0):
+def independent_pairs(n: int, rows: int = 375, cols: int = 1242, first: int = 0,
+                      px_per_cell: float = 16.0):
     """n independent stereo pairs; frame f uses seed 0x5EED0000 + f. -> (L, R) [n, rows, cols] u8."""
     L = np.empty((n, rows, cols), np.uint8)
     R = np.empty((n, rows, cols), np.uint8)
     for i in range(n):
-        L[i], R[i] = stereo_pair(SEED_BASE + first + i, rows, cols)
+        seed = SEED_BASE + first + i
+        L[i], R[i] = stereo_pair(seed, rows, cols, planes=random_scene(seed, rows, cols, px_per_cell=px_per_cell))
     return L, R
+
+
+def large_pairs(n: int, first: int = 0):
+    """BASELINE configs[4] inputs: n independent 1920x1080 pairs with ~8k keypoints per image."""
+    return independent_pairs(n, LARGE_ROWS, LARGE_COLS, first, LARGE_PX_PER_CELL)
 
 
 def yaw(deg: float) -> np.ndarray:

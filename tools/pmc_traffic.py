@@ -18,8 +18,8 @@ from collections import defaultdict
 
 # rocprofv3 kernel symbol -> libvo profiler name (bench.py roofline keys)
 RULES = [
-    (r"k_blur_stream<\d+, [15]>", "k_blur_base"),
-    (r"k_blur_stream<\d+, 0>", "k_blur_fused"),
+    (r"k_blur_stream<\d+, [15](, \d+)?>", "k_blur_base"),
+    (r"k_blur_stream<\d+, [02](, \d+)?>", "k_blur_fused"),
     (r"k_blur_pipe<", "k_blur_fused"),
     (r"k_small_pyr", "k_blur_small"),
     (r"k_base_src<true>", "k_base_src<true>"),
