@@ -10,8 +10,9 @@
 // VALU path.  The top-2 search is fused into the MFMA epilogue: each lane keeps
 // (best, idx, second) for its 16 accumulator rows, halves merge by xor
 // shuffles with a (value, index) total order, chunks of F2 merge in
-// k_match_final, which also applies MatchThreshold / MaxRatio and compacts the
-// pairs in ascending F1 order with a block prefix sum.
+// k_match_merge (one thread per F1 row), which also applies MatchThreshold /
+// MaxRatio; k_match_compact writes the pairs in ascending F1 order with a block
+// prefix sum.
 #include "vo_internal.h"
 
 namespace vo {
@@ -19,12 +20,20 @@ namespace vo {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-// (b,i,s) <- merge with (b2,i2,s2): lexicographic min on (value, index), and
-// the second smallest value of the union multiset.  Associative & commutative.
-__device__ __forceinline__ void top2_merge(float& b, int& i, float& s, float b2, int i2, float s2)
+// Ranking in the cosine domain.  The spec's SSD is sv = 2 - 2c with
+// c = ((float)dot * inv|a|) * inv|b|; sv is a non-increasing function of c, so the
+// k-th largest c maps to the k-th smallest sv, and for c >= 0.5 (sv <= 1, Sterbenz:
+// 2 - 2c is exact) it is strictly decreasing.  Every accepted match has
+// sv <= 0.04, so the argmax-c set equals the argmin-sv set there and the tie rule
+// (lowest F2 index) picks the same column; the second-best SSD is recovered as
+// 2 - 2 * (second-largest c).  Rows whose best sv > 1 may pick another index among
+// sv ties but are rejected by the threshold either way.
+// (b,i,s) <- merge with (b2,i2,s2): lexicographic max on (value, -index), and the
+// second largest value of the union multiset.  Associative & commutative.
+__device__ __forceinline__ void top2c_merge(float& b, int& i, float& s, float b2, int i2, float s2)
 {
-    const float ns = fminf(fminf(s, s2), fmaxf(b, b2));
-    if (b2 < b || (b2 == b && i2 < i)) { b = b2; i = i2; }
+    const float ns = fmaxf(fmaxf(s, s2), fminf(b, b2));
+    if (b2 > b || (b2 == b && i2 < i)) { b = b2; i = i2; }
     s = ns;
 }
 
@@ -42,6 +51,10 @@ __device__ __forceinline__ v4i load_frag(const uint8_t* row, int off)
 }
 
 // One wave per (job, 32-row F1 tile, CHUNK-column F2 chunk).  Block = 4 waves.
+// The F2 side is software-pipelined: the index of tile t+2 and the fragments +
+// metadata of tile t+1 are in flight while tile t runs its 4 MFMAs and epilogue.
+// Epilogue per accumulator element: dot = acc + 128 sa - 2^21 + 128 sb (one add3),
+// c = ((float)dot * inv|a|) * inv|b|, then a branch-free top-2 on c.
 __global__ __launch_bounds__(256) void k_match_partial(const MatchJob* __restrict__ jobs, int n_jobs,
                                                        MatchTop2* __restrict__ partial, int row_cap, int n_chunks_cap)
 {
@@ -83,50 +96,69 @@ __global__ __launch_bounds__(256) void k_match_partial(const MatchJob* __restric
                 for (int kk = 0; kk < 4; ++kk) a[kk] = (v4i){0, 0, 0, 0};
             }
         }
-        // per-accumulator-row metadata
-        int sa[16];
+        // per-accumulator-row constants
+        int rk[16];
         float ina[16];
         float best[16], second[16];
         int bidx[16];
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
             const int row = i0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            int sa = 0;
+            ina[reg] = 0.0f;
             if (row < n1) {
                 const int ra = J.idx1 ? J.idx1[row] : row;
                 const DescMeta m = J.m1[ra];
-                sa[reg] = m.sum; ina[reg] = m.inv_norm;
-            } else { sa[reg] = 0; ina[reg] = 0.0f; }
-            best[reg] = INFINITY; second[reg] = INFINITY; bidx[reg] = -1;
+                sa = m.sum; ina[reg] = m.inv_norm;
+            }
+            rk[reg] = 128 * sa - 2097152;
+            best[reg] = -INFINITY; second[reg] = -INFINITY; bidx[reg] = -1;
+        }
+        // F2 pipeline: column jc of tile jt -> descriptor row (clamped into the chunk; the
+        // epilogue masks columns >= j1)
+        auto col_row = [&](int jt) {
+            const int jc = min(jt + l31, j1 - 1);
+            return J.idx2 ? J.idx2[jc] : jc;
+        };
+        v4i bn[4];
+        int ckn, rb_next = col_row(j0 + 32 < j1 ? j0 + 32 : j0);
+        float inbn;
+        {
+            const int rb = col_row(j0);
+            const uint8_t* row = J.d2 + (size_t)rb * VO_DESC_LEN;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) bn[kk] = load_frag(row, 32 * kk + 16 * h);
+            const DescMeta m = J.m2[rb];
+            ckn = 128 * m.sum; inbn = m.inv_norm;
         }
         for (int jt = j0; jt < j1; jt += 32) {
-            const int jc = jt + l31;
-            const bool cv = jc < j1;
             v4i b[4];
-            int sb = 0;
-            float inb = 0.0f;
-            if (cv) {
-                const int rb = J.idx2 ? J.idx2[jc] : jc;
-                const uint8_t* row = J.d2 + (size_t)rb * VO_DESC_LEN;
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) b[kk] = load_frag(row, 32 * kk + 16 * h);
-                const DescMeta m = J.m2[rb];
-                sb = m.sum; inb = m.inv_norm;
-            } else {
+            for (int kk = 0; kk < 4; ++kk) b[kk] = bn[kk];
+            const int ck = ckn;
+            const float inb = inbn;
+            if (jt + 32 < j1) {                           // issue tile jt+32, and the index of jt+64
+                const uint8_t* row = J.d2 + (size_t)rb_next * VO_DESC_LEN;
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) b[kk] = (v4i){0, 0, 0, 0};
+                for (int kk = 0; kk < 4; ++kk) bn[kk] = load_frag(row, 32 * kk + 16 * h);
+                const DescMeta m = J.m2[rb_next];
+                ckn = 128 * m.sum; inbn = m.inv_norm;
+                if (jt + 64 < j1) rb_next = col_row(jt + 64);
             }
             v16i accv = (v16i){0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) accv = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kk], b[kk], accv, 0, 0, 0);
-            if (cv) {
+            const int jc = jt + l31;
+            // ragged last tile: masked columns get c = -inf (never ranked)
+            const float cmask = jc < j1 ? 0.0f : -INFINITY;
 #pragma unroll
-                for (int reg = 0; reg < 16; ++reg) {
-                    const int dot = accv[reg] + 128 * (sa[reg] + sb) - 2097152;
-                    const float c = ((float)dot * ina[reg]) * inb;
-                    const float sv = 2.0f - 2.0f * c;
-                    if (sv < best[reg]) { second[reg] = best[reg]; best[reg] = sv; bidx[reg] = jc; }
-                    else if (sv < second[reg]) second[reg] = sv;
-                }
+            for (int reg = 0; reg < 16; ++reg) {
+                const float f = (float)(accv[reg] + rk[reg] + ck);
+                const float c = (f * ina[reg]) * inb + cmask;
+                const bool gt = c > best[reg];
+                second[reg] = fmaxf(second[reg], fminf(c, best[reg]));
+                best[reg] = fmaxf(best[reg], c);
+                bidx[reg] = gt ? jc : bidx[reg];
             }
         }
         // merge the 32 lanes of each half (same accumulator rows, different columns)
@@ -137,12 +169,12 @@ __global__ __launch_bounds__(256) void k_match_partial(const MatchJob* __restric
                 const float b2 = __shfl_xor(best[reg], off);
                 const int i2 = __shfl_xor(bidx[reg], off);
                 const float s2 = __shfl_xor(second[reg], off);
-                top2_merge(best[reg], bidx[reg], second[reg], b2, i2, s2);
+                top2c_merge(best[reg], bidx[reg], second[reg], b2, i2, s2);
             }
         }
         if (l31 < 16) {
             // lane l31 of half h writes accumulator row `l31` (select by unrolled compare)
-            float bb = INFINITY, ss = INFINITY;
+            float bb = -INFINITY, ss = -INFINITY;
             int ii = -1;
 #pragma unroll
             for (int reg = 0; reg < 16; ++reg)
@@ -155,6 +187,27 @@ __global__ __launch_bounds__(256) void k_match_partial(const MatchJob* __restric
             }
         }
     }
+}
+
+// One thread per (job, F1 row): merge the F2 chunks, back to SSD, MatchThreshold and
+// MaxRatio.  res = accepted F2 index or -1.
+__global__ __launch_bounds__(256) void k_match_merge(const MatchJob* __restrict__ jobs, const MatchTop2* __restrict__ partial,
+                                                     int* __restrict__ res, int row_cap, int n_chunks_cap, float T, float max_ratio)
+{
+    const int jb = blockIdx.y, r = blockIdx.x * 256 + threadIdx.x;
+    const int n1 = job_rows(jobs[jb].n1, row_cap), n2 = job_rows(jobs[jb].n2, row_cap);
+    if (r >= n1) return;
+    const int nch = (n2 + VO_MATCH_CHUNK - 1) / VO_MATCH_CHUNK;
+    const MatchTop2* P = partial + (size_t)jb * n_chunks_cap * row_cap + r;
+    float b = -INFINITY, s = -INFINITY;
+    int i = -1;
+    for (int c = 0; c < nch; ++c) {
+        const MatchTop2 m = P[(size_t)c * row_cap];
+        top2c_merge(b, i, s, m.best, m.idx, m.second);
+    }
+    const float bs = 2.0f - 2.0f * b, ss = 2.0f - 2.0f * s;      // SSD of best / second best
+    const bool ok = i >= 0 && bs <= T && (bs / ss) <= max_ratio;
+    res[(size_t)jb * row_cap + r] = ok ? i : -1;
 }
 
 __device__ __forceinline__ uint32_t block_exscan_1024_m(uint32_t v, uint32_t* sh, uint32_t* total)
@@ -184,41 +237,23 @@ __device__ __forceinline__ uint32_t block_exscan_1024_m(uint32_t v, uint32_t* sh
     return before + x - v;
 }
 
-// One block (1024 threads) per job: merge chunks, accept, compact.
-__global__ __launch_bounds__(1024) void k_match_final(const MatchJob* __restrict__ jobs, const MatchTop2* __restrict__ partial,
-                                                      int row_cap, int n_chunks_cap, float T, float max_ratio)
+// One block (1024 threads) per job: compact the accepted rows in ascending F1 order.
+__global__ __launch_bounds__(1024) void k_match_compact(const MatchJob* __restrict__ jobs, const int* __restrict__ res, int row_cap)
 {
     __shared__ uint32_t sh[32];
     const int jb = blockIdx.x, tid = threadIdx.x;
     const MatchJob J = jobs[jb];
-    const int n1 = job_rows(J.n1, row_cap), n2 = job_rows(J.n2, row_cap);
-    const int nch = (n2 + VO_MATCH_CHUNK - 1) / VO_MATCH_CHUNK;
+    const int n1 = job_rows(J.n1, row_cap);
     const int chunk = (n1 + 1023) / 1024;
     const int a = tid * chunk, e = min(a + chunk, n1);
-    const MatchTop2* P = partial + (size_t)jb * n_chunks_cap * row_cap;
-    // pass 1: count accepted rows in my range
+    const int* R = res + (size_t)jb * row_cap;
     uint32_t cnt = 0;
-    for (int r = a; r < e; ++r) {
-        float b = INFINITY, s = INFINITY;
-        int i = -1;
-        for (int c = 0; c < nch; ++c) {
-            const MatchTop2 m = P[(size_t)c * row_cap + r];
-            top2_merge(b, i, s, m.best, m.idx, m.second);
-        }
-        const bool ok = i >= 0 && b <= T && (b / s) <= max_ratio;
-        cnt += ok;
-    }
+    for (int r = a; r < e; ++r) cnt += R[r] >= 0;
     uint32_t total;
     uint32_t base = block_exscan_1024_m(cnt, sh, &total);
     for (int r = a; r < e; ++r) {
-        float b = INFINITY, s = INFINITY;
-        int i = -1;
-        for (int c = 0; c < nch; ++c) {
-            const MatchTop2 m = P[(size_t)c * row_cap + r];
-            top2_merge(b, i, s, m.best, m.idx, m.second);
-        }
-        const bool ok = i >= 0 && b <= T && (b / s) <= max_ratio;
-        if (ok) {
+        const int i = R[r];
+        if (i >= 0) {
             if (base < (uint32_t)J.cap) { J.out_i[base] = r; J.out_j[base] = i; }
             base++;
         }
@@ -247,6 +282,7 @@ hipError_t match_alloc(MatchBuffers& b, int max_jobs, int row_cap)
     b.n_chunks = (row_cap + VO_MATCH_CHUNK - 1) / VO_MATCH_CHUNK;
     hipError_t e = hipMalloc((void**)&b.jobs, sizeof(MatchJob) * max_jobs);
     if (e != hipSuccess) return e;
+    if ((e = hipMalloc((void**)&b.res, sizeof(int) * (size_t)max_jobs * row_cap)) != hipSuccess) return e;
     return hipMalloc((void**)&b.partial, sizeof(MatchTop2) * (size_t)max_jobs * b.n_chunks * row_cap);
 }
 
@@ -254,6 +290,7 @@ void match_free(MatchBuffers& b)
 {
     hipFree(b.jobs);
     hipFree(b.partial);
+    hipFree(b.res);
     b = MatchBuffers();
 }
 
@@ -262,6 +299,7 @@ MatchBuffers match_view(const MatchBuffers& b, int k0)
     MatchBuffers v = b;
     v.jobs = b.jobs ? b.jobs + k0 : nullptr;
     v.partial = b.partial + (size_t)k0 * b.n_chunks * b.row_cap;
+    v.res = b.res + (size_t)k0 * b.row_cap;
     v.max_jobs = b.max_jobs - k0;
     return v;
 }
@@ -270,8 +308,9 @@ void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, con
 {
     if (n_jobs <= 0) return;
     VO_LAUNCH(k_match_partial, dim3(2048), dim3(256), 0, s, d_jobs, n_jobs, b.partial, b.row_cap, b.n_chunks);
-    VO_LAUNCH(k_match_final, dim3(n_jobs), dim3(1024), 0, s, d_jobs, (const MatchTop2*)b.partial, b.row_cap, b.n_chunks,
-              p.match_threshold * 0.04f, p.max_ratio);
+    VO_LAUNCH(k_match_merge, dim3((b.row_cap + 255) / 256, n_jobs), dim3(256), 0, s, d_jobs, (const MatchTop2*)b.partial,
+              b.res, b.row_cap, b.n_chunks, p.match_threshold * 0.04f, p.max_ratio);
+    VO_LAUNCH(k_match_compact, dim3(n_jobs), dim3(1024), 0, s, d_jobs, (const int*)b.res, b.row_cap);
 }
 
 void desc_meta_launch(const uint8_t* desc, DescMeta* meta, int n, hipStream_t s)

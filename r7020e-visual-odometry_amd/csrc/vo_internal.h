@@ -166,11 +166,14 @@ struct MatchJob {
     int pad;
 };
 
+// Per (row, F2 chunk) top-2 in the cosine domain: best/second are the largest
+// c = ((float)dot * inv|a|) * inv|b| values (SSD = 2 - 2c is non-increasing in c).
 struct MatchTop2 { float best; int idx; float second; int pad; };
 
 struct MatchBuffers {
     MatchJob* jobs = nullptr;        // device copy of the jobs [max_jobs]
     MatchTop2* partial = nullptr;    // [max_jobs][n_chunks][row_cap]
+    int* res = nullptr;              // [max_jobs][row_cap] accepted F2 index per F1 row, -1 if none
     int max_jobs = 0, row_cap = 0, n_chunks = 0;
 };
 
