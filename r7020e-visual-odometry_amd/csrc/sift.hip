@@ -1562,7 +1562,7 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
     const size_t lds = sizeof(float) * ft_lds_floats(K.r);
     static const int use_pipe = getenv("VO_BLUR_PIPE") ? atoi(getenv("VO_BLUR_PIPE")) : 0;
     if constexpr (MODE == 0 && RAD > 0) if (!use_pipe) {
-        static const int th_env = getenv("VO_BLUR_TH") ? atoi(getenv("VO_BLUR_TH")) : 48;
+        static const int th_env = getenv("VO_BLUR_TH") ? atoi(getenv("VO_BLUR_TH")) : 128;
         static const int wave_target = getenv("VO_BLUR_WAVES") ? atoi(getenv("VO_BLUR_WAVES")) : 1024;
         // band height: a multiple of P, at most th_env, lowered on small octaves until
         // the launch has ~wave_target waves (8 per CU) -- small planes are latency-bound
