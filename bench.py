@@ -44,10 +44,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=32, help="stereo frames per step")
+    ap.add_argument("--batch", type=int, default=64, help="stereo frames per step")
     ap.add_argument("--cpu-frames", type=int, default=10, help="frames in the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3)
+    ap.add_argument("--concurrency", type=int, default=0, help="forked streams per batch (0: library default)")
     ap.add_argument("--full-frames", type=int, default=64,
                     help="frames of the synthetic sequence timed through the full per-frame path (0: skip)")
     ap.add_argument("--large-batch", type=int, default=8,
@@ -93,6 +94,8 @@ def main():
     torch.cuda.synchronize()
 
     ctx = vo.Context(ROWS, COLS, B, device=local)
+    if args.concurrency > 0:
+        ctx.set_concurrency(args.concurrency)
     stats = ctx.sift_match_batch_dev(d_l.data_ptr(), d_r.data_ptr(), B, stats=True)
     for _ in range(args.warmup):
         ctx.sift_match_batch_dev(d_l.data_ptr(), d_r.data_ptr(), B, stats=False)

@@ -659,38 +659,50 @@ __global__ __launch_bounds__(1024) void k_lm_filter(const float* __restrict__ sp
                                                     int* __restrict__ lm_new, int* __restrict__ lm_M,
                                                     int* __restrict__ lm_rows)
 {
+    // One block per frame.  Stereo matches are taken 1024 at a time (one per thread,
+    // rounds keep the ascending order of the compaction); the old points are staged
+    // through LDS 1024 at a time and every thread compares its match against all of
+    // them (broadcast reads).  hit = any old left x == lx or any old left y == ly, or
+    // likewise on the right (VO.m:150-151, exact float equality).
     __shared__ uint32_t sh[32];
+    __shared__ float4 so[1024];
     const int f = blockIdx.x, tid = threadIdx.x, K = kp_cap;
     int S = s_n[f];
     if (S > K) S = K;
     int nk = kn[(size_t)f * kn_stride];
     if (nk > K) nk = K;
     if (nk < 0) nk = 0;
-    const float* sp = spos + (size_t)f * K * 4;
-    const float* op = oldpos + (size_t)f * K * 4;
+    const float4* sp = reinterpret_cast<const float4*>(spos + (size_t)f * K * 4);
+    const float4* op = reinterpret_cast<const float4*>(oldpos + (size_t)f * K * 4);
     uint8_t* fl = flags + (size_t)f * K;
-    const int chunk = (S + 1023) / 1024;
-    const int a0 = tid * chunk, e = min(a0 + chunk, S);
-    uint32_t cnt = 0;
-    for (int j = a0; j < e; ++j) {
-        const float lx = sp[4 * j], ly = sp[4 * j + 1], rx = sp[4 * j + 2], ry = sp[4 * j + 3];
+    uint32_t done = 0;                                      // new landmarks emitted by earlier rounds
+    for (int j0 = 0; j0 < S; j0 += 1024) {
+        const int j = j0 + tid;
+        const bool valid = j < S;
+        const float4 p = valid ? sp[j] : float4{0.0f, 0.0f, 0.0f, 0.0f};
         bool hit = false;
-        for (int k = 0; k < nk && !hit; ++k)
-            if (op[4 * k] == lx || op[4 * k + 1] == ly) hit = true;
-        for (int k = 0; k < nk && !hit; ++k)
-            if (op[4 * k + 2] == rx || op[4 * k + 3] == ry) hit = true;
-        fl[j] = hit ? 0 : 1;
-        cnt += hit ? 0 : 1;
+        for (int k0 = 0; k0 < nk; k0 += 1024) {
+            __syncthreads();
+            if (k0 + tid < nk) so[tid] = op[k0 + tid];
+            __syncthreads();
+            const int kc = min(1024, nk - k0);
+            for (int k = 0; k < kc; ++k) {
+                const float4 o = so[k];
+                hit = hit | (o.x == p.x) | (o.y == p.y) | (o.z == p.z) | (o.w == p.w);
+            }
+        }
+        const uint32_t isnew = (valid && !hit) ? 1u : 0u;
+        if (valid) fl[j] = (uint8_t)isnew;
+        uint32_t total;
+        const uint32_t pos = block_exscan_1024_g(isnew, sh, &total);
+        if (isnew) lm_new[(size_t)f * K + done + pos] = j;
+        done += total;
     }
-    uint32_t total;
-    uint32_t base = block_exscan_1024_g(cnt, sh, &total);
-    for (int j = a0; j < e; ++j)
-        if (fl[j]) lm_new[(size_t)f * K + base++] = j;
     __syncthreads();
     if (tid == 0) {
-        lm_M[f] = (int)total;
+        lm_M[f] = (int)done;
         lm_rows[f] = 2;                                     // zeros(size(features_l,2),3): 2 rows
-        for (int m = (int)total; m < 2; ++m) fl[m] = 0;     // rows beyond M stay zero rows
+        for (int m = (int)done; m < 2; ++m) fl[m] = 0;      // rows beyond M stay zero rows
     }
 }
 

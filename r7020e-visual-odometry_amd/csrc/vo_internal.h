@@ -80,7 +80,9 @@ struct Pyramid {
     int n_seg;                                // 1024-word compaction segments per image
 };
 
+#ifndef VO_EXT_BAND
 #define VO_EXT_BAND 30            // interior rows per extremum-test wave (a multiple of 3)
+#endif
 #define VO_SEG_WORDS 1024
 
 // Packed candidate: c | r << 12 | layer << 24 | o << 27  (c, r < 4096)

@@ -100,7 +100,7 @@ def load_library(path: str | os.PathLike | None = None):
     global _lib
     if _lib is not None:
         return _lib
-    p = Path(path) if path else LIBPATH
+    p = Path(path) if path else Path(os.environ.get("VO_LIBPATH", LIBPATH))
     if not p.exists():
         raise VOError(VO_ERR_STATE, f"{p} not built; run __graft_entry__.build() (make -C csrc)")
     # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same
