@@ -680,17 +680,28 @@ __global__ __launch_bounds__(1024) void k_lm_filter(const float* __restrict__ sp
         const int j = j0 + tid;
         const bool valid = j < S;
         const float4 p = valid ? sp[j] : float4{0.0f, 0.0f, 0.0f, 0.0f};
-        bool hit = false;
+        // one lane-mask accumulator per coordinate (v_cmp + s_or per compare); 8 LDS
+        // reads in flight per unrolled step; slots past the chunk end hold NaN (never equal)
+        bool hx = false, hy = false, hz = false, hw = false;
         for (int k0 = 0; k0 < nk; k0 += 1024) {
             __syncthreads();
-            if (k0 + tid < nk) so[tid] = op[k0 + tid];
+            so[tid] = k0 + tid < nk ? op[k0 + tid] : float4{NAN, NAN, NAN, NAN};
             __syncthreads();
-            const int kc = min(1024, nk - k0);
-            for (int k = 0; k < kc; ++k) {
-                const float4 o = so[k];
-                hit = hit | (o.x == p.x) | (o.y == p.y) | (o.z == p.z) | (o.w == p.w);
+            const int kc = (min(1024, nk - k0) + 7) & ~7;
+            for (int k = 0; k < kc; k += 8) {
+                float4 o[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) o[u] = so[k + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    hx |= o[u].x == p.x;
+                    hy |= o[u].y == p.y;
+                    hz |= o[u].z == p.z;
+                    hw |= o[u].w == p.w;
+                }
             }
         }
+        const bool hit = hx || hy || hz || hw;
         const uint32_t isnew = (valid && !hit) ? 1u : 0u;
         if (valid) fl[j] = (uint8_t)isnew;
         uint32_t total;

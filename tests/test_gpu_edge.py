@@ -1,0 +1,91 @@
+"""GPU parity on edge cases: odd and tiny image sizes (including KITTI-00's real
+376x1241), a blank image (no keypoints), and matchFeatures on empty, single-row,
+duplicate and ragged descriptor sets (sizes that are not multiples of the 32-row
+MFMA tile or the 512-column F2 chunk).  Everything is compared bit for bit with
+the CPU oracle."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [(376, 1241), (120, 200), (77, 101), (64, 64), (33, 47)]
+
+
+def _same_kps(a, b):
+    assert len(a) == len(b), (len(a), len(b))
+    for f in ("x", "y", "size", "angle", "response", "octave", "layer", "scale"):
+        assert np.array_equal(a[f], b[f]), f
+
+
+@pytest.mark.parametrize("rows,cols", SIZES)
+def test_sift_odd_sizes_bit_exact(vo, oracle, syn, rows, cols):
+    import torch
+    L, R = syn.stereo_pair(syn.SEED_BASE + 31, rows, cols)
+    ctx = vo.Context(rows, cols, 2)
+    k, d = ctx.sift(L)
+    rk, rd = oracle.sift(L)
+    _same_kps(k, rk)
+    assert np.array_equal(d, rd)
+    # batch path: two frames (the second is the first mirrored), stereo matches included
+    Ls = np.ascontiguousarray(np.stack([L, L[:, ::-1]]))
+    Rs = np.ascontiguousarray(np.stack([R, R[:, ::-1]]))
+    dl, dr = torch.from_numpy(Ls).cuda(), torch.from_numpy(Rs).cuda()
+    torch.cuda.synchronize()
+    ctx.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), 2)
+    for f in range(2):
+        kl, dsl = ctx.fetch_keypoints(2 * f)
+        kr, dsr = ctx.fetch_keypoints(2 * f + 1)
+        rkl, rdl = oracle.sift(Ls[f])
+        rkr, rdr = oracle.sift(Rs[f])
+        _same_kps(kl, rkl)
+        _same_kps(kr, rkr)
+        assert np.array_equal(dsl, rdl) and np.array_equal(dsr, rdr)
+        assert np.array_equal(ctx.fetch_stereo_pairs(f), oracle.match(rdl, rdr))
+    ctx.close()
+
+
+def test_blank_image_has_no_keypoints(vo):
+    import torch
+    Z = np.zeros((1, 100, 160), np.uint8)
+    ctx = vo.Context(100, 160, 1)
+    k, d = ctx.sift(Z[0])
+    assert len(k) == 0 and d.shape == (0, 128)
+    dz = torch.from_numpy(Z).cuda()
+    torch.cuda.synchronize()
+    stats = ctx.sift_match_batch_dev(dz.data_ptr(), dz.data_ptr(), 1)
+    assert tuple(stats[0][:3]) == (0, 0, 0)
+    assert len(ctx.fetch_stereo_pairs(0)) == 0
+    ctx.close()
+
+
+def test_match_edge_cases_bit_exact(vo, oracle):
+    rng = np.random.default_rng(5)
+    F = rng.integers(0, 100, (10, 128)).astype(np.uint8)
+    ctx = vo.Context(375, 1242, 1)
+    cases = [
+        (F, F[:0]), (F[:0], F),                       # empty sides
+        (F, F[3:4]),                                  # a single candidate: ratio test passes
+        (F, F),                                       # identity pairs
+        (F[:1], np.vstack([F[:1], F[:1]])),           # exact duplicate best: 0/0 ratio, rejected
+        (F, np.vstack([F[5:6], F, F[5:6]])),          # duplicates among many
+    ]
+    for F1, F2 in cases:
+        got = ctx.match(F1, F2)
+        ref = oracle.match(F1, F2)
+        assert np.array_equal(got, ref), (F1.shape, F2.shape)
+    assert ctx.match(F, F[3:4]).tolist() == [[4, 1]]
+    ctx.close()
+
+
+@pytest.mark.parametrize("n1,n2", [(1, 1), (31, 33), (33, 511), (513, 513), (1025, 1100), (70, 2049)])
+def test_match_ragged_sizes_bit_exact(vo, oracle, n1, n2):
+    rng = np.random.default_rng(n1 * 7919 + n2)
+    base = rng.integers(0, 140, (max(n1, n2) + 64, 128)).astype(np.uint8)
+    F1 = base[:n1].copy()
+    # F2: noisy copies of a shifted window of the same rows, so many rows have a true match
+    F2 = np.clip(base[32:32 + n2].astype(int) + rng.integers(-4, 5, (n2, 128)), 0, 255).astype(np.uint8)
+    ctx = vo.Context(375, 1242, 1)
+    got = ctx.match(F1, F2)
+    ref = oracle.match(F1, F2)
+    assert np.array_equal(got, ref)
+    ctx.close()
