@@ -12,7 +12,7 @@ Prints ONE JSON line (rank 0) with the driver's contract fields plus
 `roofline` (dominant kernel, HIP-event durations measured in this process)
 and `cpu_baseline` (the CPU oracle on a bounded sample, rank 0 at N=1).
 `full_path` additionally times the full per-frame path (vo_step_batch_dev) over
-a synthetic moving-camera sequence (--full-frames, default 64; 0 skips), and
+a synthetic moving-camera sequence (--full-frames, default 256; 0 skips), and
 `large` the 1920x1080 / ~8k keypoint configuration (configs[4]) per GPU with the
 i8-MFMA rate of its dense stereo match block (--large-batch, default 8; 0 skips).
 """
@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3)
     ap.add_argument("--concurrency", type=int, default=0, help="forked streams per batch (0: library default)")
-    ap.add_argument("--full-frames", type=int, default=64,
+    ap.add_argument("--full-frames", type=int, default=256,
                     help="frames of the synthetic sequence timed through the full per-frame path (0: skip)")
     ap.add_argument("--large-batch", type=int, default=8,
                     help="1920x1080 (~8k keypoints) stereo pairs per step for the configs[4] figure (0: skip)")
@@ -170,13 +170,15 @@ def main():
     # sequence, frames chained across batches of B (device-resident inputs) ----
     full = None
     if args.full_frames > 0:
-        nf = args.full_frames // B * B
-        # ping-pong walk (0.25 m/frame forward, then back) keeps the fronto-parallel planes
-        # of the synthetic scene in view, so keypoint counts stay near the ~2k of configs[1]
-        half = (nf + 1) // 2
-        SL, SR, _gt = syn.sequence(half, ROWS, COLS, seed=syn.SEED_BASE + 0x100 * rank, step_m=0.25, yaw_deg=0.1)
-        SL = np.ascontiguousarray(np.concatenate([SL, SL[::-1]])[:nf])
-        SR = np.ascontiguousarray(np.concatenate([SR, SR[::-1]])[:nf])
+        nf = max(1, args.full_frames // B) * B
+        # ping-pong walk (0.25 m/frame forward for 32 frames, then back) keeps the
+        # fronto-parallel planes of the synthetic scene in view, so keypoint counts stay near
+        # the ~2k of configs[1]; the 64-frame loop repeats (frame 64k is frame 0 again)
+        SL, SR, _gt = syn.sequence(32, ROWS, COLS, seed=syn.SEED_BASE + 0x100 * rank, step_m=0.25, yaw_deg=0.1)
+        loop = np.arange(nf) % 64
+        loop = np.where(loop < 32, loop, 63 - loop)
+        SL = np.ascontiguousarray(SL[loop])
+        SR = np.ascontiguousarray(SR[loop])
         d_sl = torch.from_numpy(SL).to(f"cuda:{local}")
         d_sr = torch.from_numpy(SR).to(f"cuda:{local}")
         P1, P2 = syn.calib()
@@ -184,10 +186,16 @@ def main():
         fs = SL[0].size
 
         def run_seq():
+            # pipelined loop body (vo_step_submit_dev / vo_step_collect): batch k+1's SIFT
+            # overlaps batch k's tracking / MSAC / landmarks and its host pose chain
             fctx.reset()
             outs = []
             for b0 in range(0, nf, B):
-                outs.append(fctx.step_batch_dev(d_sl.data_ptr() + b0 * fs, d_sr.data_ptr() + b0 * fs, B))
+                fctx.step_submit_dev(d_sl.data_ptr() + b0 * fs, d_sr.data_ptr() + b0 * fs, B)
+                if fctx.steps_pending() == 2:
+                    outs.append(fctx.step_collect())
+            while fctx.steps_pending():
+                outs.append(fctx.step_collect())
             return np.concatenate(outs)
 
         run_seq()
@@ -206,8 +214,8 @@ def main():
                 "value": nf * reps * world / fel, "unit": "stereo frames/s", "frames_per_rank": nf, "batch": B,
                 "ransac_hypotheses": 2048, "frames_with_pose": int(ok.sum()), "mean_inliers": float(outs["n_inliers"][1:].mean()),
                 "mean_keypoints_per_image": float((outs["n_left"] + outs["n_right"]).mean() / 2),
-                "note": "frames chained through vo_step_batch_dev (tracking carried across batches); "
-                        "includes the per-batch pose/landmark download and host pose chain"}
+                "note": "frames chained through vo_step_submit_dev/vo_step_collect (tracking carried across "
+                        "batches, two batches in flight); includes the per-batch pose/landmark download and host pose chain"}
         fctx.close()
         del d_sl, d_sr
 

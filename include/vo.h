@@ -23,6 +23,8 @@
  *                          CreateLandmarksFromFeatures.m:1-21
  *   vo_step / vo_step_batch the whole loop body VO.m:70-161 (features stay
  *                          device-resident between frames)
+ *   vo_step_submit_dev /   the same loop body, pipelined: batch n+1's SIFT
+ *   vo_step_collect        overlaps batch n's geometry and host pose chain
  *   vo_sift_match_batch    VO.m:79-87 for a batch of independent stereo pairs
  *                          (the benchmark workload, BASELINE.json configs[1])
  *
@@ -194,6 +196,18 @@ int vo_step_batch(vo_ctx* ctx, const uint8_t* lefts, const uint8_t* rights, int 
 /* Same, inputs already in device memory (tightly packed rows*cols each). */
 int vo_step_batch_dev(vo_ctx* ctx, const uint8_t* d_lefts, const uint8_t* d_rights, int B,
                       vo_step_out* outs);
+
+/* Pipelined form of vo_step_batch_dev (same results, bit for bit).  submit enqueues the
+ * device half of B frames and returns; collect waits for the oldest submitted batch and
+ * runs the host half (pose chain, landmark append), writing its B outputs.  Consecutive
+ * batches alternate two buffer sets, so batch n+1's SIFT overlaps batch n's tracking /
+ * MSAC / landmark kernels and the host work of collect(n).  At most two batches may be
+ * pending (submit(n+2) needs collect(n) first); other calls on the context are refused
+ * while any is pending.  Inputs of a submit made while another batch is pending must be
+ * ready on the device at the call (the first submit is ordered after vo_stream()). */
+int vo_step_submit_dev(vo_ctx* ctx, const uint8_t* d_lefts, const uint8_t* d_rights, int B);
+int vo_step_collect(vo_ctx* ctx, vo_step_out* outs, int capacity, int* n);
+int vo_steps_pending(const vo_ctx* ctx);
 
 /* Landmarks accumulated so far ([rows][3] double, world frame). */
 int vo_get_landmarks(vo_ctx* ctx, double* out, int capacity, int* rows);

@@ -7,6 +7,7 @@
 #include <cstdarg>
 #include <string>
 #include <vector>
+#include <deque>
 #include <algorithm>
 
 namespace vo {
@@ -73,11 +74,15 @@ struct vo_ctx {
     // buffer sets; set 0 is the context's own buffers (sb, mb, stereo jobs, pairs), set 1
     // is `aux`.  A call's scale space waits only for the previous use of its own set, so
     // the pyramid of call N+1 overlaps the latency-bound feature stages of call N.
+    // Set 1 is a full replica of set 0's per-frame state (image slots incl. the carried
+    // frame, pair slots incl. the carry slot, stereo + tracking jobs, geometry buffers), so
+    // the full per-frame path can also alternate sets (vo_step_submit_dev).
     struct AuxSet {
         SiftBuffers sb;
         MatchBuffers mb;
-        MatchJob* d_jobs = nullptr;
-        int* pair_i = nullptr; int* pair_j = nullptr; int* pair_n = nullptr;
+        MatchJob* d_jobs = nullptr;      // [0, M) stereo, [M, 5M) tracking (job_track layout)
+        int* pair_i = nullptr; int* pair_j = nullptr; int* pair_n = nullptr;   // max_batch + 1 slots
+        GeomBuffers gb;
     } aux;
     hipEvent_t ev_done[2] = {};
     int next_set = 0, last_set = 0;
@@ -96,6 +101,17 @@ struct vo_ctx {
     int* d_fn = nullptr;             // [2]
     int* d_mi = nullptr; int* d_mj = nullptr; int* d_mn = nullptr;
     GeomBuffers gb;
+    // Pipelined full path (vo_step_submit_dev / vo_step_collect): batch n uses buffer set
+    // n & 1; its geometry runs on `stream` while the next batch's SIFT runs on sub[0..1].
+    // Per set: pinned host copies of the per-frame results and the event that ends the
+    // batch (geometry, carry into the other set, result copies).
+    struct StepHost { FrameGeom* fg = nullptr; int* nkp = nullptr; int* np = nullptr; int* rows = nullptr; };
+    StepHost sh[2];
+    hipEvent_t ev_step[2] = {};
+    hipStream_t copy_stream = nullptr;
+    struct Pending { int set, B; bool first_tracked; };
+    std::deque<Pending> pending;
+    int next_step_set = 0;
     std::string err;
     Profiler prof;
     int last_B = 0;
@@ -156,8 +172,11 @@ static void destroy_streams(vo_ctx* c)
     c->ev_fork = nullptr;
     for (int k = 0; k < 2; ++k) {
         if (c->ev_done[k]) hipEventDestroy(c->ev_done[k]);
-        c->ev_done[k] = nullptr;
+        if (c->ev_step[k]) hipEventDestroy(c->ev_step[k]);
+        c->ev_done[k] = nullptr; c->ev_step[k] = nullptr;
     }
+    if (c->copy_stream) hipStreamDestroy(c->copy_stream);
+    c->copy_stream = nullptr;
 }
 
 static void destroy_buffers(vo_ctx* c)
@@ -167,6 +186,11 @@ static void destroy_buffers(vo_ctx* c)
     sift_free(c->aux.sb);
     match_free(c->aux.mb);
     hipFree(c->aux.d_jobs); hipFree(c->aux.pair_i); hipFree(c->aux.pair_j); hipFree(c->aux.pair_n);
+    geom_free(c->aux.gb);
+    for (int k = 0; k < 2; ++k) {
+        hipHostFree(c->sh[k].fg); hipHostFree(c->sh[k].nkp); hipHostFree(c->sh[k].np); hipHostFree(c->sh[k].rows);
+        c->sh[k] = vo_ctx::StepHost();
+    }
     geom_free(c->gb);
     hipFree(c->d_py); hipFree(c->d_jobs); hipFree(c->d_pair_i); hipFree(c->d_pair_j); hipFree(c->d_pair_n);
     hipFree(c->d_img); hipFree(c->d_fd[0]); hipFree(c->d_fd[1]); hipFree(c->d_fm[0]); hipFree(c->d_fm[1]);
@@ -208,8 +232,11 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
         if ((e = hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
     }
     if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("event", e);
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < 2; ++k) {
         if ((e = hipEventCreateWithFlags(&c->ev_done[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
+        if ((e = hipEventCreateWithFlags(&c->ev_step[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
+    }
+    if ((e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking)) != hipSuccess) return bail("stream", e);
     const int n_slots = 2 * max_batch + 2;
     const int kp_cap = c->sp.max_keypoints;
     build_pyramid_geometry(c->py, rows, cols, n_slots, c->sp);
@@ -255,18 +282,20 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
         J.out_i = c->d_mi; J.out_j = c->d_mj; J.out_n = c->d_mn; J.cap = kp_cap;
     }
     if ((e = hipMemcpy(c->d_jobs, jobs.data(), sizeof(MatchJob) * n_jobs, hipMemcpyHostToDevice)) != hipSuccess) return bail("jobs copy", e);
-    // second buffer set of the asynchronous batch pipeline (stereo frames only)
+    // second buffer set of the asynchronous pipelines (a full replica of set 0's per-frame state)
     {
         vo_ctx::AuxSet& X = c->aux;
+        const int xn = 5 * max_batch;
         if ((e = sift_alloc(X.sb, c->py, kp_cap, 4 * kp_cap)) != hipSuccess) return bail("sift buffers (set 1)", e);
         if ((e = match_alloc(X.mb, max_batch, kp_cap)) != hipSuccess) return bail("match buffers (set 1)", e);
-        if ((e = hipMalloc((void**)&X.d_jobs, sizeof(MatchJob) * max_batch)) != hipSuccess) return bail("jobs (set 1)", e);
-        if ((e = hipMalloc((void**)&X.pair_i, sizeof(int) * (size_t)max_batch * kp_cap)) != hipSuccess) return bail("pairs", e);
-        if ((e = hipMalloc((void**)&X.pair_j, sizeof(int) * (size_t)max_batch * kp_cap)) != hipSuccess) return bail("pairs", e);
-        if ((e = hipMalloc((void**)&X.pair_n, sizeof(int) * max_batch)) != hipSuccess) return bail("pairs", e);
-        if ((e = hipMemset(X.pair_n, 0, sizeof(int) * max_batch)) != hipSuccess) return bail("pairs", e);
-        std::vector<MatchJob> xj(max_batch);
-        memset(xj.data(), 0, sizeof(MatchJob) * max_batch);
+        if ((e = hipMalloc((void**)&X.d_jobs, sizeof(MatchJob) * xn)) != hipSuccess) return bail("jobs (set 1)", e);
+        if ((e = hipMalloc((void**)&X.pair_i, sizeof(int) * (size_t)pair_slots * kp_cap)) != hipSuccess) return bail("pairs", e);
+        if ((e = hipMalloc((void**)&X.pair_j, sizeof(int) * (size_t)pair_slots * kp_cap)) != hipSuccess) return bail("pairs", e);
+        if ((e = hipMalloc((void**)&X.pair_n, sizeof(int) * pair_slots)) != hipSuccess) return bail("pairs", e);
+        if ((e = hipMemset(X.pair_n, 0, sizeof(int) * pair_slots)) != hipSuccess) return bail("pairs", e);
+        if ((e = geom_alloc(X.gb, max_batch, kp_cap, c->rp.max_num_trials)) != hipSuccess) return bail("geometry buffers (set 1)", e);
+        std::vector<MatchJob> xj(xn);
+        memset(xj.data(), 0, sizeof(MatchJob) * xn);
         for (int f = 0; f < max_batch; ++f) {
             MatchJob& J = xj[f];
             const int il = 2 * f, ir = 2 * f + 1;
@@ -275,8 +304,16 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
             J.out_i = X.pair_i + (size_t)f * kp_cap; J.out_j = X.pair_j + (size_t)f * kp_cap; J.out_n = X.pair_n + f;
             J.cap = kp_cap;
         }
-        if ((e = hipMemcpy(X.d_jobs, xj.data(), sizeof(MatchJob) * max_batch, hipMemcpyHostToDevice)) != hipSuccess)
+        geom_fill_track_jobs(X.gb, xj.data(), max_batch, job_track(c, 0, 0), X.sb, X.pair_i, X.pair_j, X.pair_n, kp_cap);
+        if ((e = hipMemcpy(X.d_jobs, xj.data(), sizeof(MatchJob) * xn, hipMemcpyHostToDevice)) != hipSuccess)
             return bail("jobs copy (set 1)", e);
+    }
+    for (int k = 0; k < 2; ++k) {
+        vo_ctx::StepHost& H = c->sh[k];
+        if ((e = hipHostMalloc((void**)&H.fg, sizeof(FrameGeom) * max_batch, 0)) != hipSuccess) return bail("pinned", e);
+        if ((e = hipHostMalloc((void**)&H.nkp, sizeof(int) * 2 * max_batch, 0)) != hipSuccess) return bail("pinned", e);
+        if ((e = hipHostMalloc((void**)&H.np, sizeof(int) * max_batch, 0)) != hipSuccess) return bail("pinned", e);
+        if ((e = hipHostMalloc((void**)&H.rows, sizeof(int) * max_batch, 0)) != hipSuccess) return bail("pinned", e);
     }
     return c;
 }
@@ -349,19 +386,25 @@ static int finish(vo_ctx* c)
 }
 // quiesce: calls that run on `stream` over the context's own buffers first wait for any
 // batch still in flight on either buffer set (no host synchronisation)
-static void begin_call(vo_ctx* c, bool quiesce = true)
+// Calls other than the step pipeline's own are refused while step batches are pending
+// (they reuse buffer set 0).
+static int begin_call(vo_ctx* c, bool quiesce = true, bool step = false)
 {
     hipSetDevice(c->device);
+    if (!step && !c->pending.empty())
+        return fail(c, VO_ERR_STATE, "asynchronous step batches pending (vo_step_collect first)");
     g_prof = c->prof.on ? &c->prof : nullptr;
     if (quiesce)
         for (int k = 0; k < 2; ++k) hipStreamWaitEvent(c->stream, c->ev_done[k], 0);
+    return VO_OK;
 }
+#define BEGIN_CALL(...) do { int rc_ = begin_call(__VA_ARGS__); if (rc_) return rc_; } while (0)
 
 int vo_sift(vo_ctx* c, const uint8_t* img, int rows, int cols, int ld, vo_keypoint* kps, uint8_t* desc, int capacity,
             int* n_out)
 {
     if (!c || !img || rows != c->rows || cols != c->cols || ld < cols) return fail(c, VO_ERR_ARG, "vo_sift: bad arguments");
-    begin_call(c);
+    BEGIN_CALL(c);
     HIPC(c, hipMemcpy2DAsync(c->d_img, cols, img, ld, cols, rows, hipMemcpyHostToDevice, c->stream));
     ImageSrc src{c->d_img, c->d_img, (size_t)rows * cols, cols, 0};
     sift_enqueue(c->py, c->sb, src, 1, c->sp, c->stream, c->d_py);
@@ -384,7 +427,7 @@ int vo_match(vo_ctx* c, const uint8_t* F1, int n1, const uint8_t* F2, int n2, ui
 {
     if (!c || n1 < 0 || n2 < 0 || (n1 && !F1) || (n2 && !F2)) return fail(c, VO_ERR_ARG, "vo_match: bad arguments");
     if (n1 > c->sb.kp_cap || n2 > c->sb.kp_cap) return fail(c, VO_ERR_CAPACITY, "vo_match: more rows than max_keypoints");
-    begin_call(c);
+    BEGIN_CALL(c);
     int nn[2] = {n1, n2};
     if (n1) HIPC(c, hipMemcpyAsync(c->d_fd[0], F1, (size_t)n1 * VO_DESC_LEN, hipMemcpyHostToDevice, c->stream));
     if (n2) HIPC(c, hipMemcpyAsync(c->d_fd[1], F2, (size_t)n2 * VO_DESC_LEN, hipMemcpyHostToDevice, c->stream));
@@ -410,11 +453,17 @@ int vo_match(vo_ctx* c, const uint8_t* F1, int n1, const uint8_t* F2, int n2, ui
 
 // SIFT + stereo match on B frames already in device memory.
 // buffers of set `set` of the asynchronous batch pipeline
-struct SetRef { SiftBuffers* sb; MatchBuffers* mb; MatchJob* jobs; int* pair_i; int* pair_j; int* pair_n; };
+struct SetRef {
+    SiftBuffers* sb; MatchBuffers* mb; MatchJob* jobs; int* pair_i; int* pair_j; int* pair_n;
+    GeomBuffers* gb; MatchJob* track_jobs;
+};
 static SetRef set_ref(vo_ctx* c, int set)
 {
-    if (set == 0) return {&c->sb, &c->mb, c->d_jobs + job_stereo(c, 0), c->d_pair_i, c->d_pair_j, c->d_pair_n};
-    return {&c->aux.sb, &c->aux.mb, c->aux.d_jobs, c->aux.pair_i, c->aux.pair_j, c->aux.pair_n};
+    if (set == 0)
+        return {&c->sb, &c->mb, c->d_jobs + job_stereo(c, 0), c->d_pair_i, c->d_pair_j, c->d_pair_n, &c->gb,
+                c->d_jobs + job_track(c, 0, 0)};
+    return {&c->aux.sb, &c->aux.mb, c->aux.d_jobs, c->aux.pair_i, c->aux.pair_j, c->aux.pair_n, &c->aux.gb,
+            c->aux.d_jobs + job_track(c, 0, 0)};
 }
 
 // SIFT of 2B images + stereo matching of B frames into buffer set `set`.  The frames are
@@ -423,14 +472,17 @@ static SetRef set_ref(vo_ctx* c, int set)
 // features of part k overlap the scale space of part k+1 (and of the next call, which uses
 // the other set).  Inputs are ordered after earlier work on `stream`; the set's previous
 // contents are released by its ev_done.  With `join`, `stream` waits for the result.
-static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uint8_t* d_r, int B, bool join)
+static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uint8_t* d_r, int B, bool join,
+                               bool fork = true)
 {
     const size_t fs = (size_t)c->rows * c->cols;
     const int parts = std::min(c->n_sub, B);
     SetRef S = set_ref(c, set);
     hipStream_t sp = c->sub[0], st = c->sub[1];
-    HIPC(c, hipEventRecord(c->ev_fork, c->stream));           // inputs / earlier work on `stream`
-    HIPC(c, hipStreamWaitEvent(sp, c->ev_fork, 0));
+    if (fork) {                                                 // inputs / earlier work on `stream`
+        HIPC(c, hipEventRecord(c->ev_fork, c->stream));
+        HIPC(c, hipStreamWaitEvent(sp, c->ev_fork, 0));
+    }
     HIPC(c, hipStreamWaitEvent(sp, c->ev_done[set], 0));      // set free (its previous features done)
     for (int p = 0; p < parts; ++p) {
         const int f0 = B * p / parts, nf = B * (p + 1) / parts - f0;
@@ -455,7 +507,7 @@ static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uin
 int vo_sift_match_batch_dev(vo_ctx* c, const uint8_t* d_lefts, const uint8_t* d_rights, int B, vo_pair_stats* stats)
 {
     if (!c || !d_lefts || !d_rights || B < 1 || B > c->max_batch) return fail(c, VO_ERR_ARG, "vo_sift_match_batch_dev: bad arguments");
-    begin_call(c, false);
+    BEGIN_CALL(c, false);
     const int set = c->next_set;
     c->next_set ^= 1;
     const bool sync = stats != nullptr;      // profiling events are collected by vo_kernel_times
@@ -535,11 +587,12 @@ static vo_calib calib_of(const double P1[12], const double P2[12], const double*
     return c;
 }
 
-static StepArgs step_args(vo_ctx* c, int B)
+static StepArgs step_args(vo_ctx* c, int B, int set = 0)
 {
+    SetRef S = set_ref(c, set);
     StepArgs a;
-    a.sb = &c->sb;
-    a.pair_i = c->d_pair_i; a.pair_j = c->d_pair_j; a.pair_n = c->d_pair_n;
+    a.sb = S.sb;
+    a.pair_i = S.pair_i; a.pair_j = S.pair_j; a.pair_n = S.pair_n;
     a.max_frames = c->max_batch; a.B = B; a.kp_cap = c->sb.kp_cap;
     a.first_has_prev = c->have_features ? 1 : 0;
     a.frame_index0 = c->frame_index;
@@ -568,69 +621,105 @@ static void lm_world(const double* pose, const float* X, double* out)
 }
 
 // copy frame f's SIFT results + stereo pairs into the carry slots (prev of the next call's frame 0)
-static int enqueue_carry(vo_ctx* c, int f)
+// Frame f of set `from` becomes the carried (previous) frame of set `to`: its keypoints,
+// descriptors and stereo pairs are copied into `to`'s carry slots (image slots 2M, 2M+1,
+// pair slot M), which frame 0 of the next batch tracks against.
+static int enqueue_carry(vo_ctx* c, int from, int f, int to)
 {
     const int M = c->max_batch, K = c->sb.kp_cap;
+    SetRef A = set_ref(c, from), Z = set_ref(c, to);
     for (int side = 0; side < 2; ++side) {
         const int src = 2 * f + side, dst = 2 * M + side;
-        HIPC(c, hipMemcpyAsync(c->sb.kp + (size_t)dst * K, c->sb.kp + (size_t)src * K, sizeof(vo_keypoint) * K,
+        HIPC(c, hipMemcpyAsync(Z.sb->kp + (size_t)dst * K, A.sb->kp + (size_t)src * K, sizeof(vo_keypoint) * K,
                                hipMemcpyDeviceToDevice, c->stream));
-        HIPC(c, hipMemcpyAsync(c->sb.desc + (size_t)dst * K * VO_DESC_LEN, c->sb.desc + (size_t)src * K * VO_DESC_LEN,
+        HIPC(c, hipMemcpyAsync(Z.sb->desc + (size_t)dst * K * VO_DESC_LEN, A.sb->desc + (size_t)src * K * VO_DESC_LEN,
                                (size_t)K * VO_DESC_LEN, hipMemcpyDeviceToDevice, c->stream));
-        HIPC(c, hipMemcpyAsync(c->sb.meta + (size_t)dst * K, c->sb.meta + (size_t)src * K, sizeof(DescMeta) * K,
+        HIPC(c, hipMemcpyAsync(Z.sb->meta + (size_t)dst * K, A.sb->meta + (size_t)src * K, sizeof(DescMeta) * K,
                                hipMemcpyDeviceToDevice, c->stream));
-        HIPC(c, hipMemcpyAsync(c->sb.n_kp + dst, c->sb.n_kp + src, sizeof(int), hipMemcpyDeviceToDevice, c->stream));
+        HIPC(c, hipMemcpyAsync(Z.sb->n_kp + dst, A.sb->n_kp + src, sizeof(int), hipMemcpyDeviceToDevice, c->stream));
     }
-    HIPC(c, hipMemcpyAsync(c->d_pair_i + (size_t)M * K, c->d_pair_i + (size_t)f * K, sizeof(int) * K, hipMemcpyDeviceToDevice, c->stream));
-    HIPC(c, hipMemcpyAsync(c->d_pair_j + (size_t)M * K, c->d_pair_j + (size_t)f * K, sizeof(int) * K, hipMemcpyDeviceToDevice, c->stream));
-    HIPC(c, hipMemcpyAsync(c->d_pair_n + M, c->d_pair_n + f, sizeof(int), hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(Z.pair_i + (size_t)M * K, A.pair_i + (size_t)f * K, sizeof(int) * K, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(Z.pair_j + (size_t)M * K, A.pair_j + (size_t)f * K, sizeof(int) * K, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(Z.pair_n + M, A.pair_n + f, sizeof(int), hipMemcpyDeviceToDevice, c->stream));
     return VO_OK;
 }
 
-// The VO.m loop body for B frames whose images are in device memory.
-static int run_batch(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B, vo_step_out* outs)
+// The VO.m loop body for B frames whose images are in device memory, split into a
+// device half (submit: everything up to the per-frame results, asynchronous) and a host
+// half (collect: pose chain VO.m:130-134 and landmark append CreateLandmarksFromFeatures.m:20).
+// Batch n uses buffer set n & 1.  Its SIFT + stereo matching run on sub[0..1] and wait only
+// for the previous batch of the same set (collected before this submit); its tracking,
+// triangulation, MSAC and landmark kernels run on `stream` after the SIFT and after the
+// previous batch's carry; then frame B-1 is carried into the other set and the small
+// per-frame results are copied to pinned host memory.  With fork, the SIFT is also ordered
+// after earlier work on `stream` (the synchronous calls' H2D copies).
+static int submit_batch(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B, bool fork)
 {
     if (!c->has_calib) return fail(c, VO_ERR_STATE, "vo_step: no calibration (vo_set_calib)");
-    const int K = c->sb.kp_cap;
-    int rc0 = enqueue_sift_stereo(c, 0, d_l, d_r, B, true);       // buffer set 0, joined into `stream`
-    if (rc0) return rc0;
-    StepArgs a = step_args(c, B);
-    geom_enqueue(c->gb, c->mb, c->d_jobs + job_track(c, 0, 0), a, c->mp, c->stream);
-    std::vector<FrameGeom> fg(B);
-    std::vector<int> nkp(2 * B), np(B), rows(B);
-    HIPC(c, hipMemcpyAsync(fg.data(), c->gb.fg, sizeof(FrameGeom) * B, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipMemcpyAsync(nkp.data(), c->sb.n_kp, sizeof(int) * 2 * B, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipMemcpyAsync(np.data(), c->d_pair_n, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipMemcpyAsync(rows.data(), c->gb.lm_rows, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
-    int rc = enqueue_carry(c, B - 1);
+    if (c->pending.size() >= 2) return fail(c, VO_ERR_STATE, "vo_step_submit_dev: two batches already pending (collect first)");
+    const int set = c->next_step_set;
+    SetRef S = set_ref(c, set);
+    int rc = enqueue_sift_stereo(c, set, d_l, d_r, B, true, fork);   // `stream` waits for this set's SIFT
     if (rc) return rc;
-    rc = finish(c);
-    if (rc) return rc;
+    StepArgs a = step_args(c, B, set);
+    geom_enqueue(*S.gb, *S.mb, S.track_jobs, a, c->mp, c->stream);
+    vo_ctx::StepHost& H = c->sh[set];
+    HIPC(c, hipMemcpyAsync(H.fg, S.gb->fg, sizeof(FrameGeom) * B, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(H.nkp, S.sb->n_kp, sizeof(int) * 2 * B, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(H.np, S.pair_n, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(H.rows, S.gb->lm_rows, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
+    if ((rc = enqueue_carry(c, set, B - 1, set ^ 1))) return rc;
+    HIPC(c, hipEventRecord(c->ev_step[set], c->stream));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(c, VO_ERR_HIP, "launch: %s", hipGetErrorString(e));
+    c->pending.push_back({set, B, c->have_features});
+    c->next_step_set ^= 1;
+    c->have_features = true;
+    c->frame_index += B;
+    return VO_OK;
+}
+
+static int collect_batch(vo_ctx* c, vo_step_out* outs, int capacity, int* n_out)
+{
+    if (c->pending.empty()) return fail(c, VO_ERR_STATE, "vo_step_collect: no batch pending");
+    const vo_ctx::Pending P = c->pending.front();
+    if (capacity < P.B) return fail(c, VO_ERR_CAPACITY, "vo_step_collect: %d frames pending, capacity %d", P.B, capacity);
+    const int K = c->sb.kp_cap, B = P.B;
+    SetRef S = set_ref(c, P.set);
+    const vo_ctx::StepHost& H = c->sh[P.set];
+    if (c->prof.on) {                                  // profiling: events of every stream are collected
+        g_prof = &c->prof;
+        int rc = finish(c);
+        if (rc) return rc;
+    } else {
+        HIPC(c, hipEventSynchronize(c->ev_step[P.set]));
+    }
     std::vector<std::vector<float>> X(B);
     std::vector<std::vector<uint8_t>> keep(B);
     for (int f = 0; f < B; ++f) {
-        int r = std::min(rows[f], K);
+        int r = std::min(H.rows[f], K);
         X[f].resize((size_t)r * 3);
         keep[f].resize(r);
         if (r > 0) {
-            HIPC(c, hipMemcpyAsync(X[f].data(), c->gb.lm_X + (size_t)f * K * 3, sizeof(float) * 3 * r, hipMemcpyDeviceToHost, c->stream));
-            HIPC(c, hipMemcpyAsync(keep[f].data(), c->gb.lm_keep + (size_t)f * K, r, hipMemcpyDeviceToHost, c->stream));
+            HIPC(c, hipMemcpyAsync(X[f].data(), S.gb->lm_X + (size_t)f * K * 3, sizeof(float) * 3 * r, hipMemcpyDeviceToHost, c->copy_stream));
+            HIPC(c, hipMemcpyAsync(keep[f].data(), S.gb->lm_keep + (size_t)f * K, r, hipMemcpyDeviceToHost, c->copy_stream));
         }
     }
-    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipStreamSynchronize(c->copy_stream));
+    c->pending.pop_front();
     for (int f = 0; f < B; ++f) {
         vo_step_out& o = outs[f];
         memset(&o, 0, sizeof(o));
-        o.n_left = nkp[2 * f]; o.n_right = nkp[2 * f + 1]; o.n_stereo = np[f];
+        o.n_left = H.nkp[2 * f]; o.n_right = H.nkp[2 * f + 1]; o.n_stereo = H.np[f];
         memcpy(o.rel_pose, I4, sizeof(I4));
-        const bool tracked = f > 0 || c->have_features;
+        const bool tracked = f > 0 || P.first_tracked;
         if (tracked) {
-            o.status = fg[f].status;
-            o.n_tracked = fg[f].n_tracked;
-            o.n_inliers = fg[f].n_inliers;
+            o.status = H.fg[f].status;
+            o.n_tracked = H.fg[f].n_tracked;
+            o.n_inliers = H.fg[f].n_inliers;
             if (o.status == VO_OK) {
-                memcpy(o.rel_pose, fg[f].T, sizeof(fg[f].T));
-                mat4_mul(c->pose, fg[f].T, c->pose);
+                memcpy(o.rel_pose, H.fg[f].T, sizeof(H.fg[f].T));
+                mat4_mul(c->pose, H.fg[f].T, c->pose);
             }
             const int r = (int)keep[f].size();
             o.n_landmarks = r;
@@ -641,9 +730,17 @@ static int run_batch(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B, v
         }
         memcpy(o.pose, c->pose, sizeof(c->pose));
     }
-    c->have_features = true;
-    c->frame_index += B;
+    if (n_out) *n_out = B;
     return VO_OK;
+}
+
+// synchronous form: submit + collect (nothing else may be pending)
+static int run_batch(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B, vo_step_out* outs)
+{
+    if (!c->pending.empty()) return fail(c, VO_ERR_STATE, "vo_step: asynchronous batches pending (vo_step_collect first)");
+    int rc = submit_batch(c, d_l, d_r, B, true);
+    if (rc) return rc;
+    return collect_batch(c, outs, B, nullptr);
 }
 
 extern "C" {
@@ -651,7 +748,7 @@ extern "C" {
 int vo_step_batch_dev(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B, vo_step_out* outs)
 {
     if (!c || !d_l || !d_r || !outs || B < 1 || B > c->max_batch) return fail(c, VO_ERR_ARG, "vo_step_batch_dev: bad arguments");
-    begin_call(c);
+    BEGIN_CALL(c);
     int rc = run_batch(c, d_l, d_r, B, outs);
     g_prof = nullptr;
     return rc;
@@ -661,7 +758,7 @@ int vo_step_batch(vo_ctx* c, const uint8_t* lefts, const uint8_t* rights, int ld
 {
     if (!c || !lefts || !rights || !outs || B < 1 || B > c->max_batch || ld < c->cols)
         return fail(c, VO_ERR_ARG, "vo_step_batch: bad arguments");
-    begin_call(c);
+    BEGIN_CALL(c);
     const size_t fs = (size_t)c->rows * c->cols;
     uint8_t* dl = c->d_img;
     uint8_t* dr = c->d_img + fs * B;
@@ -677,6 +774,28 @@ int vo_step(vo_ctx* c, const uint8_t* left, const uint8_t* right, int ld, vo_ste
     return vo_step_batch(c, left, right, ld, 1, out);
 }
 
+int vo_step_submit_dev(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B)
+{
+    if (!c || !d_l || !d_r || B < 1 || B > c->max_batch) return fail(c, VO_ERR_ARG, "vo_step_submit_dev: bad arguments");
+    BEGIN_CALL(c, false, true);
+    // the first batch of a pipeline is ordered after earlier work on `stream`; later ones
+    // overlap the previous batch's geometry (their inputs must be ready at the call)
+    int rc = submit_batch(c, d_l, d_r, B, c->pending.empty());
+    if (!c->prof.on) g_prof = nullptr;
+    return rc;
+}
+
+int vo_step_collect(vo_ctx* c, vo_step_out* outs, int capacity, int* n)
+{
+    if (!c || !outs) return fail(c, VO_ERR_ARG, "vo_step_collect: bad arguments");
+    hipSetDevice(c->device);
+    int rc = collect_batch(c, outs, capacity, n);
+    g_prof = nullptr;
+    return rc;
+}
+
+int vo_steps_pending(const vo_ctx* c) { return c ? (int)c->pending.size() : 0; }
+
 int vo_get_landmarks(vo_ctx* c, double* out, int capacity, int* rows)
 {
     if (!c) return VO_ERR_ARG;
@@ -690,12 +809,15 @@ int vo_reset(vo_ctx* c)
 {
     if (!c) return VO_ERR_ARG;
     hipSetDevice(c->device);
-    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipDeviceSynchronize());                   // drops any pending asynchronous batches
+    c->pending.clear();
+    c->next_step_set = 0;
     c->have_features = false;
     c->frame_index = 0;
     memcpy(c->pose, I4, sizeof(I4));
     c->landmarks.clear();
     HIPC(c, hipMemset(c->d_pair_n + c->max_batch, 0, sizeof(int)));
+    HIPC(c, hipMemset(c->aux.pair_n + c->max_batch, 0, sizeof(int)));
     return VO_OK;
 }
 
@@ -724,7 +846,7 @@ int vo_track(vo_ctx* c, const uint8_t* old_l, const uint8_t* old_r, int n_old, c
     if (!c || n_old < 0 || n_cl < 0 || n_cr < 0) return fail(c, VO_ERR_ARG, "vo_track: bad arguments");
     const int K = c->sb.kp_cap, M = c->max_batch;
     if (n_old > K || n_cl > K || n_cr > K) return fail(c, VO_ERR_CAPACITY, "vo_track: more rows than max_keypoints");
-    begin_call(c);
+    BEGIN_CALL(c);
     c->have_features = false;
     int rc;
     if ((rc = upload_desc(c, 2 * M, old_l, n_old))) return rc;
@@ -764,7 +886,7 @@ int vo_track(vo_ctx* c, const uint8_t* old_l, const uint8_t* old_r, int n_old, c
 int vo_triangulate(vo_ctx* c, const float* x1, const float* x2, int n, const double P1[12], const double P2[12], double* X)
 {
     if (!c || n < 0 || (n && (!x1 || !x2 || !X)) || !P1 || !P2) return fail(c, VO_ERR_ARG, "vo_triangulate: bad arguments");
-    begin_call(c);
+    BEGIN_CALL(c);
     const vo_calib cal = calib_of(P1, P2, nullptr);
     const int K = c->sb.kp_cap;
     std::vector<float> q((size_t)std::min(n, K) * 4 + 4);
@@ -794,7 +916,7 @@ int vo_estworldpose(vo_ctx* c, const double* img, const double* world, int n, co
     if (rp.max_num_trials > c->gb.n_hyp) return fail(c, VO_ERR_ARG, "vo_estworldpose: max_num_trials > context's");
     if (n_inliers) *n_inliers = 0;
     if (n < 4) return fail(c, VO_ERR_TOO_FEW_POINTS, "estworldpose: need at least 4 points, got %d", n);
-    begin_call(c);
+    BEGIN_CALL(c);
     c->have_features = false;
     HIPC(c, hipMemcpyAsync(c->gb.imgpt, img, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipMemcpyAsync(c->gb.world, world, sizeof(double) * 3 * n, hipMemcpyHostToDevice, c->stream));
@@ -820,7 +942,7 @@ int vo_landmarks(vo_ctx* c, const float* l_pos, const float* r_pos, int S, const
     if (!c->has_calib) return fail(c, VO_ERR_STATE, "vo_landmarks: no calibration");
     const int K = c->sb.kp_cap;
     if (S > K || Kn > K) return fail(c, VO_ERR_CAPACITY, "vo_landmarks: more rows than max_keypoints");
-    begin_call(c);
+    BEGIN_CALL(c);
     c->have_features = false;
     std::vector<float> sp((size_t)S * 4 + 4), op((size_t)Kn * 4 + 4);
     for (int j = 0; j < S; ++j) { sp[4 * j] = l_pos[2 * j]; sp[4 * j + 1] = l_pos[2 * j + 1]; sp[4 * j + 2] = r_pos[2 * j]; sp[4 * j + 3] = r_pos[2 * j + 1]; }

@@ -87,7 +87,8 @@ STEP_DTYPE = np.dtype([("status", "<i4"), ("n_left", "<i4"), ("n_right", "<i4"),
 EXPORTS = [
     "vo_default_sift_params", "vo_default_match_params", "vo_default_ransac_params", "vo_create", "vo_destroy",
     "vo_set_calib", "vo_last_error", "vo_sift", "vo_match", "vo_track", "vo_triangulate", "vo_estworldpose",
-    "vo_landmarks", "vo_step", "vo_step_batch", "vo_step_batch_dev", "vo_get_landmarks", "vo_reset",
+    "vo_landmarks", "vo_step", "vo_step_batch", "vo_step_batch_dev", "vo_step_submit_dev", "vo_step_collect",
+    "vo_steps_pending", "vo_get_landmarks", "vo_reset",
     "vo_sift_match_batch_dev", "vo_fetch_keypoints", "vo_fetch_stereo_pairs", "vo_stream", "vo_set_profiling",
     "vo_kernel_times", "vo_set_frame_index", "vo_set_concurrency",
 ]
@@ -136,6 +137,9 @@ def load_library(path: str | os.PathLike | None = None):
     L.vo_step.argtypes = [vp, P(C.c_uint8), P(C.c_uint8), C.c_int, P(StepOut)]
     L.vo_step_batch.argtypes = [vp, P(C.c_uint8), P(C.c_uint8), C.c_int, C.c_int, P(StepOut)]
     L.vo_step_batch_dev.argtypes = [vp, vp, vp, C.c_int, P(StepOut)]
+    L.vo_step_submit_dev.argtypes = [vp, vp, vp, C.c_int]
+    L.vo_step_collect.argtypes = [vp, P(StepOut), C.c_int, P(C.c_int)]
+    L.vo_steps_pending.argtypes = [vp]
     L.vo_get_landmarks.argtypes = [vp, P(C.c_double), C.c_int, P(C.c_int)]
     L.vo_reset.argtypes = [vp]
     L.vo_set_frame_index.argtypes = [vp, C.c_long]
@@ -332,6 +336,20 @@ class Context:
         self._check(self.lib.vo_step_batch_dev(self.h, C.c_void_p(d_lefts), C.c_void_p(d_rights), B,
                                                outs.ctypes.data_as(C.POINTER(StepOut))))
         return outs
+
+    def step_submit_dev(self, d_lefts: int, d_rights: int, B: int) -> None:
+        """Pipelined step_batch_dev, device half (vo_step_submit_dev): returns at once."""
+        self._check(self.lib.vo_step_submit_dev(self.h, C.c_void_p(d_lefts), C.c_void_p(d_rights), B))
+
+    def step_collect(self) -> np.ndarray:
+        """Outputs of the oldest submitted batch (vo_step_collect)."""
+        outs = np.zeros(self.max_batch, STEP_DTYPE)
+        n = C.c_int(0)
+        self._check(self.lib.vo_step_collect(self.h, outs.ctypes.data_as(C.POINTER(StepOut)), self.max_batch, C.byref(n)))
+        return outs[: n.value].copy()
+
+    def steps_pending(self) -> int:
+        return int(self.lib.vo_steps_pending(self.h))
 
     def step(self, left: np.ndarray, right: np.ndarray):
         return self.step_batch(left[None], right[None])[0]

@@ -139,3 +139,45 @@ def test_sequence_stepwise_bit_exact(vo, oracle, syn, seq, calib):
     ctx.reset()
     outs2 = np.array([ctx.step(L[f], R[f]) for f in range(n)], dtype=routs.dtype)
     _compare_seq(outs2, ctx.get_landmarks(), routs, rlm)
+
+
+def test_sequence_pipelined_bit_exact(vo, oracle, syn, seq, calib):
+    """vo_step_submit_dev / vo_step_collect (two buffer sets, batch n+1's SIFT overlapping
+    batch n's geometry) give the oracle's VO.m loop bit for bit, with ragged batches."""
+    import torch
+    L, R, _ = seq
+    routs, rlm = oracle.run_sequence(L, R, syn.KITTI00_P0, syn.KITTI00_P1)
+    ctx = vo.Context(375, 1242, 3, calib=calib)
+    dl, dr = torch.from_numpy(np.ascontiguousarray(L)).cuda(), torch.from_numpy(np.ascontiguousarray(R)).cuda()
+    torch.cuda.synchronize()
+    fs = L[0].size
+    bounds = [(0, 2), (2, 3), (3, 6)]
+    outs = []
+    for k, (a, b) in enumerate(bounds):
+        ctx.step_submit_dev(dl.data_ptr() + a * fs, dr.data_ptr() + a * fs, b - a)
+        if k >= 1:
+            outs.append(ctx.step_collect())
+    while ctx.steps_pending():
+        outs.append(ctx.step_collect())
+    _compare_seq(np.concatenate(outs), ctx.get_landmarks(), routs, rlm)
+    # pipeline rules: at most two batches pending, other calls refused meanwhile
+    ctx.reset()
+    ctx.step_submit_dev(dl.data_ptr(), dr.data_ptr(), 1)
+    ctx.step_submit_dev(dl.data_ptr() + fs, dr.data_ptr() + fs, 1)
+    with pytest.raises(vo.VOError):
+        ctx.step_submit_dev(dl.data_ptr() + 2 * fs, dr.data_ptr() + 2 * fs, 1)
+    with pytest.raises(vo.VOError):
+        ctx.step_batch_dev(dl.data_ptr(), dr.data_ptr(), 1)
+    ctx.step_collect()
+    ctx.step_collect()
+    with pytest.raises(vo.VOError):
+        ctx.step_collect()
+    # reset drops pending work; the synchronous form still works afterwards
+    ctx.reset()
+    ctx.step_submit_dev(dl.data_ptr(), dr.data_ptr(), 3)
+    ctx.reset()
+    assert ctx.steps_pending() == 0
+    s1 = ctx.step_batch_dev(dl.data_ptr(), dr.data_ptr(), 3)
+    s2 = ctx.step_batch_dev(dl.data_ptr() + 3 * fs, dr.data_ptr() + 3 * fs, 3)
+    _compare_seq(np.concatenate([s1, s2]), ctx.get_landmarks(), routs, rlm)
+    ctx.close()

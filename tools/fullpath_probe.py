@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel breakdown of the full per-frame path (BASELINE configs[2] on the synthetic
 sequence bench.py uses): wall time per batch and libvo's HIP-event kernel times.
-usage: python tools/fullpath_probe.py [frames] [batch]"""
+usage: python tools/fullpath_probe.py [frames] [batch] [pipe]"""
 import sys
 import time
 from pathlib import Path
@@ -24,9 +24,21 @@ ctx = vo.Context(375, 1242, B, calib=vo.calib_from(P1, P2))
 fs = SL[0].size
 
 
+PIPE = len(sys.argv) > 3 and sys.argv[3] == "pipe"
+
+
 def run():
     ctx.reset()
-    return np.concatenate([ctx.step_batch_dev(dl.data_ptr() + b * fs, dr.data_ptr() + b * fs, B) for b in range(0, nf, B)])
+    if not PIPE:
+        return np.concatenate([ctx.step_batch_dev(dl.data_ptr() + b * fs, dr.data_ptr() + b * fs, B) for b in range(0, nf, B)])
+    outs = []
+    for b in range(0, nf, B):
+        ctx.step_submit_dev(dl.data_ptr() + b * fs, dr.data_ptr() + b * fs, B)
+        if ctx.steps_pending() == 2:
+            outs.append(ctx.step_collect())
+    while ctx.steps_pending():
+        outs.append(ctx.step_collect())
+    return np.concatenate(outs)
 
 
 run()
