@@ -201,9 +201,32 @@ class KittiSequence:
         self._pool.shutdown(wait=True)
 
 
+def _pipelined(ctx, batches, dev) -> list:
+    """Drive the loop body through vo_step_submit_dev / vo_step_collect: while batch n's
+    kernels run, the host decodes and uploads batch n+1 (threaded PNG decode, pinned H2D),
+    and batch n+1's SIFT overlaps batch n's geometry.  Input tensors stay referenced until
+    their batch is collected."""
+    import torch
+    outs, inflight = [], []
+    for _b0, L, R in batches:
+        dl = torch.from_numpy(L).pin_memory().to(dev, non_blocking=True)
+        dr = torch.from_numpy(R).pin_memory().to(dev, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()         # inputs ready before the submit
+        ctx.step_submit_dev(dl.data_ptr(), dr.data_ptr(), L.shape[0])
+        inflight.append((dl, dr))
+        if ctx.steps_pending() == 2:
+            outs.append(ctx.step_collect())
+            inflight.pop(0)
+    while ctx.steps_pending():
+        outs.append(ctx.step_collect())
+        inflight.pop(0)
+    return outs
+
+
 def run(seq: KittiSequence, batch: int = 16, stop: int | None = None, device: int = 0, ctx=None):
     """The VO.m loop over a KITTI sequence through libvo: frames in batches of `batch`
-    (vo_step_batch_dev, tracking carried across batches), H2D from pinned host buffers.
+    (pipelined vo_step_submit_dev / vo_step_collect, tracking carried across batches), H2D
+    from pinned host buffers.
     Returns (poses [n, 4, 4] with frame 0 = identity, per-frame vo_step_out records,
     landmarks [L, 3])."""
     import torch
@@ -211,15 +234,7 @@ def run(seq: KittiSequence, batch: int = 16, stop: int | None = None, device: in
     own = ctx is None
     if own:
         ctx = vo.Context(seq.rows, seq.cols, batch, device=device, calib=vo.calib_from(seq.P1, seq.P2))
-    outs = []
-    dev = torch.device("cuda", device)
-    for _b0, L, R in seq.batches(batch, 0, stop):
-        hl = torch.from_numpy(L).pin_memory()
-        hr = torch.from_numpy(R).pin_memory()
-        dl = hl.to(dev, non_blocking=True)
-        dr = hr.to(dev, non_blocking=True)
-        torch.cuda.current_stream(dev).synchronize()
-        outs.append(ctx.step_batch_dev(dl.data_ptr(), dr.data_ptr(), L.shape[0]))
+    outs = _pipelined(ctx, seq.batches(batch, 0, stop), torch.device("cuda", device))
     outs = np.concatenate(outs) if outs else np.zeros(0, vo.STEP_DTYPE)
     poses = np.stack([o["pose"] for o in outs]) if len(outs) else np.zeros((0, 4, 4))
     lm = ctx.get_landmarks()
@@ -241,13 +256,7 @@ def run_shard(seq: KittiSequence, rank: int, world: int, batch: int = 16, device
     ctx = vo.Context(seq.rows, seq.cols, batch, device=device, calib=vo.calib_from(seq.P1, seq.P2))
     ctx.reset()
     ctx.set_frame_index(h)
-    dev = torch.device("cuda", device)
-    outs = []
-    for _b0, L, R in seq.batches(batch, h, e):
-        dl = torch.from_numpy(L).pin_memory().to(dev, non_blocking=True)
-        dr = torch.from_numpy(R).pin_memory().to(dev, non_blocking=True)
-        torch.cuda.current_stream(dev).synchronize()
-        outs.append(ctx.step_batch_dev(dl.data_ptr(), dr.data_ptr(), L.shape[0]))
+    outs = _pipelined(ctx, seq.batches(batch, h, e), torch.device("cuda", device))
     ctx.close()
     outs = np.concatenate(outs)
     return outs["rel_pose"][s - h:]
