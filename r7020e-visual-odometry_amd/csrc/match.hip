@@ -19,6 +19,7 @@ namespace vo {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+typedef float vo_f2 __attribute__((ext_vector_type(2)));
 
 // Ranking in the cosine domain.  The spec's SSD is sv = 2 - 2c with
 // c = ((float)dot * inv|a|) * inv|b|; sv is a non-increasing function of c, so the
@@ -50,37 +51,63 @@ __device__ __forceinline__ v4i load_frag(const uint8_t* row, int off)
     return v;
 }
 
-// One wave per (job, 32-row F1 tile, CHUNK-column F2 chunk).  Block = 4 waves.
-// The F2 side is software-pipelined: the index of tile t+2 and the fragments +
-// metadata of tile t+1 are in flight while tile t runs its 4 MFMAs and epilogue.
-// Epilogue per accumulator element: dot = acc + 128 sa - 2^21 + 128 sb (one add3),
-// c = ((float)dot * inv|a|) * inv|b|, then a branch-free top-2 on c.
-__global__ __launch_bounds__(256) void k_match_partial(const MatchJob* __restrict__ jobs, int n_jobs,
+// One workgroup (4 waves) per (job, 128-row F1 block, CHUNK-column F2 chunk); wave w owns
+// F1 rows [128 blk + 32 w, +32).  The F2 side is shared: each 32-column tile (4 KB of
+// descriptors + metadata) is loaded once per workgroup, one 16-B load per thread, staged
+// through a double-buffered LDS tile, and read by every wave as MFMA B fragments.  Tile t+1
+// is written to LDS and tile t+2 is in flight from HBM/L2 while tile t runs its 4 MFMAs
+// and epilogue.  Epilogue per accumulator element: dot = acc + 128 sa - 2^21 + 128 sb (one
+// add3), c = ((float)dot * inv|a|) * inv|b| (packed muls, two rows at once), then the top-2
+// update, skipped by the wave when no lane's c beats its row's second best.
+#define MP_ROWS 128
+#define MP_LDS_ROW 144
+#define VO_MP_MAX_JOBS 256        // jobs per launch (one per thread of the task-table prologue)
+#ifndef VO_MP_BLOCKS
+#define VO_MP_BLOCKS 3            // workgroups per CU the register budget is sized for
+#endif
+__global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const MatchJob* __restrict__ jobs, int n_jobs,
                                                        MatchTop2* __restrict__ partial, int row_cap, int n_chunks_cap)
 {
-    const int lane = threadIdx.x & 63, h = lane >> 5, l31 = lane & 31;
-    const long wave0 = (long)blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = (long)gridDim.x * 4;
-    // total tasks
-    long total = 0;
-    for (int j = 0; j < n_jobs; ++j) {
-        const int n1 = job_rows(jobs[j].n1, row_cap), n2 = job_rows(jobs[j].n2, row_cap);
-        total += (long)((n1 + 31) / 32) * ((n2 + VO_MATCH_CHUNK - 1) / VO_MATCH_CHUNK);
-    }
-    for (long t = wave0; t < total; t += nwaves) {
-        // locate job
-        int jb = 0, n1 = 0, n2 = 0, nch = 0;
-        long acc = 0, rel = 0;
-        for (int j = 0; j < n_jobs; ++j) {
-            n1 = job_rows(jobs[j].n1, row_cap);
-            n2 = job_rows(jobs[j].n2, row_cap);
-            nch = (n2 + VO_MATCH_CHUNK - 1) / VO_MATCH_CHUNK;
-            const long nt = (long)((n1 + 31) / 32) * nch;
-            if (t < acc + nt) { jb = j; rel = t - acc; break; }
-            acc += nt;
+    // F2 tile rows padded to 144 B (36 dwords): the 32 lanes of a half read 16 B at row l31,
+    // so a 128-B stride would put them all on the same banks
+    __shared__ __attribute__((aligned(16))) uint8_t bt[2][32 * MP_LDS_ROW];
+    __shared__ int bck[2][32];
+    __shared__ float binb[2][32];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l31 = lane & 31;
+    const int lr = tid >> 3, lseg = tid & 7;              // loader: row lr of the tile, bytes [16 lseg, +16)
+    // task table: job j owns tasks [tstart[j], tstart[j+1]); job sizes are read on device
+    // (counts of earlier kernels), one thread per job, then a block prefix sum
+    __shared__ int tstart[VO_MP_MAX_JOBS + 1], jn1[VO_MP_MAX_JOBS], jnch[VO_MP_MAX_JOBS];
+    __shared__ int wsum[4];
+    {
+        int my = 0;
+        if (tid < n_jobs) {
+            const int n1 = job_rows(jobs[tid].n1, row_cap), n2 = job_rows(jobs[tid].n2, row_cap);
+            const int nch = (n2 + VO_MATCH_CHUNK - 1) / VO_MATCH_CHUNK;
+            jn1[tid] = n1; jnch[tid] = nch;
+            my = ((n1 + MP_ROWS - 1) / MP_ROWS) * nch;
         }
+        int inc = my;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(inc, o); if (lane >= o) inc += y; }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        int before = 0;
+        for (int w = 0; w < wave; ++w) before += wsum[w];
+        if (tid < n_jobs) tstart[tid] = before + inc - my;
+        if (tid == 255) tstart[min(n_jobs, VO_MP_MAX_JOBS)] = before + inc;
+        __syncthreads();
+    }
+    const int total = tstart[n_jobs];
+    for (int t = blockIdx.x; t < total; t += gridDim.x) {       // workgroup-uniform
+        int jb = 0;
+        while (jb + 1 < n_jobs && tstart[jb + 1] <= t) ++jb;
+        const int n1 = jn1[jb], nch = jnch[jb];
+        const int n2 = job_rows(jobs[jb].n2, row_cap);
+        const long rel = t - tstart[jb];
         const MatchJob J = jobs[jb];
-        const int tile = (int)(rel / nch), chunk = (int)(rel - (long)tile * nch);
-        const int i0 = tile * 32, j0 = chunk * VO_MATCH_CHUNK;
+        const int blk = (int)(rel / nch), chunk = (int)(rel - (long)blk * nch);
+        const int i0 = blk * MP_ROWS + 32 * wave, j0 = chunk * VO_MATCH_CHUNK;
         const int j1 = min(j0 + VO_MATCH_CHUNK, n2);
         // A fragments: F1 row i0 + l31, bytes [32kk + 16h, +16)
         v4i a[4];
@@ -96,7 +123,6 @@ __global__ __launch_bounds__(256) void k_match_partial(const MatchJob* __restric
                 for (int kk = 0; kk < 4; ++kk) a[kk] = (v4i){0, 0, 0, 0};
             }
         }
-        // per-accumulator-row constants
         int rk[16];
         float ina[16];
         float best[16], second[16];
@@ -114,51 +140,80 @@ __global__ __launch_bounds__(256) void k_match_partial(const MatchJob* __restric
             rk[reg] = 128 * sa - 2097152;
             best[reg] = -INFINITY; second[reg] = -INFINITY; bidx[reg] = -1;
         }
-        // F2 pipeline: column jc of tile jt -> descriptor row (clamped into the chunk; the
-        // epilogue masks columns >= j1)
-        auto col_row = [&](int jt) {
-            const int jc = min(jt + l31, j1 - 1);
-            return J.idx2 ? J.idx2[jc] : jc;
+        // loader: column jt + lr (clamped into the chunk; the epilogue masks columns >= j1)
+        v4i gv;
+        DescMeta gm;
+        auto gload = [&](int jt) {
+            const int jc = min(jt + lr, j1 - 1);
+            const int rb = J.idx2 ? J.idx2[jc] : jc;
+            gv = *reinterpret_cast<const v4i*>(J.d2 + (size_t)rb * VO_DESC_LEN + 16 * lseg);
+            if (lseg == 0) gm = J.m2[rb];
         };
-        v4i bn[4];
-        int ckn, rb_next = col_row(j0 + 32 < j1 ? j0 + 32 : j0);
-        float inbn;
-        {
-            const int rb = col_row(j0);
-            const uint8_t* row = J.d2 + (size_t)rb * VO_DESC_LEN;
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) bn[kk] = load_frag(row, 32 * kk + 16 * h);
-            const DescMeta m = J.m2[rb];
-            ckn = 128 * m.sum; inbn = m.inv_norm;
-        }
-        for (int jt = j0; jt < j1; jt += 32) {
-            v4i b[4];
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) b[kk] = bn[kk];
-            const int ck = ckn;
-            const float inb = inbn;
-            if (jt + 32 < j1) {                           // issue tile jt+32, and the index of jt+64
-                const uint8_t* row = J.d2 + (size_t)rb_next * VO_DESC_LEN;
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk) bn[kk] = load_frag(row, 32 * kk + 16 * h);
-                const DescMeta m = J.m2[rb_next];
-                ckn = 128 * m.sum; inbn = m.inv_norm;
-                if (jt + 64 < j1) rb_next = col_row(jt + 64);
+        // After tiles 1, 2, 4, 8, ... of the chunk every lane's second best of a row is raised
+        // to the max over the 32 lanes of the half (the row's wave-wide second best so far).
+        // The merged top-2 is unchanged: each lane's second is a candidate value other than
+        // its own best, so every second (raised or not) is <= the row's true second, which
+        // the merge still finds.  A value <= the raised second can never enter the row's final
+        // top-2 (later columns only lose ties), so the wave skips the update unless some lane
+        // beats its second -- rare once the row has settled.
+        int tno = 0;
+        auto lstore = [&](int buf) {                       // stored as b - 128 (the MFMA operand)
+            *reinterpret_cast<v4i*>(&bt[buf][lr * MP_LDS_ROW + 16 * lseg]) =
+                gv ^ (v4i){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
+            if (lseg == 0) { bck[buf][lr] = 128 * gm.sum; binb[buf][lr] = gm.inv_norm; }
+        };
+        gload(j0);
+        __syncthreads();                                   // previous task's readers are done with bt
+        lstore(0);
+        if (j0 + 32 < j1) gload(j0 + 32);
+        int buf = 0;
+        for (int jt = j0; jt < j1; jt += 32, buf ^= 1) {
+            __syncthreads();                               // tile jt visible; tile jt-32's buffer free
+            if (jt + 32 < j1) {
+                lstore(buf ^ 1);                           // tile jt+32 (loaded one iteration ago)
+                if (jt + 64 < j1) gload(jt + 64);
             }
+            v4i b[4];
+            const uint8_t* brow = &bt[buf][l31 * MP_LDS_ROW + 16 * h];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) b[kk] = *reinterpret_cast<const v4i*>(brow + 32 * kk);
+            const int ck = bck[buf][l31];
+            const float inb = binb[buf][l31];
             v16i accv = (v16i){0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) accv = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kk], b[kk], accv, 0, 0, 0);
             const int jc = jt + l31;
-            // ragged last tile: masked columns get c = -inf (never ranked)
+            // ragged last tile: masked columns get c = -inf (never ranked); elsewhere c + 0 = c
+            // exactly (c >= +0)
             const float cmask = jc < j1 ? 0.0f : -INFINITY;
 #pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
-                const float f = (float)(accv[reg] + rk[reg] + ck);
-                const float c = (f * ina[reg]) * inb + cmask;
-                const bool gt = c > best[reg];
-                second[reg] = fmaxf(second[reg], fminf(c, best[reg]));
-                best[reg] = fmaxf(best[reg], c);
-                bidx[reg] = gt ? jc : bidx[reg];
+            for (int reg = 0; reg < 16; reg += 2) {
+                // c for two accumulator rows at once: the two products as packed f32 muls
+                // (each component an IEEE multiply, same bits as the scalar form)
+                const vo_f2 fp = vo_f2{(float)(accv[reg] + rk[reg] + ck), (float)(accv[reg + 1] + rk[reg + 1] + ck)};
+                vo_f2 cp = (fp * vo_f2{ina[reg], ina[reg + 1]}) * vo_f2{inb, inb};
+                cp = cp + vo_f2{cmask, cmask};
+#pragma unroll
+                for (int h2 = 0; h2 < 2; ++h2) {
+                    const int q = reg + h2;
+                    const float c = h2 ? cp.y : cp.x;
+                    if (__builtin_amdgcn_ballot_w64(c > second[q])) {
+                        const bool g1 = c > best[q], g2 = c > second[q];
+                        second[q] = g1 ? best[q] : (g2 ? c : second[q]);
+                        best[q] = g1 ? c : best[q];
+                        bidx[q] = g1 ? jc : bidx[q];
+                    }
+                }
+            }
+            ++tno;
+            if ((tno & (tno - 1)) == 0) {                  // wave-uniform
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg) {
+                    float m = second[reg];
+#pragma unroll
+                    for (int off = 16; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+                    second[reg] = m;
+                }
             }
         }
         // merge the 32 lanes of each half (same accumulator rows, different columns)
@@ -307,6 +362,11 @@ MatchBuffers match_view(const MatchBuffers& b, int k0)
 void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, const vo_match_params& p, hipStream_t s)
 {
     if (n_jobs <= 0) return;
+    if (n_jobs > VO_MP_MAX_JOBS) {                       // the task table holds VO_MP_MAX_JOBS jobs
+        match_launch(b, d_jobs, VO_MP_MAX_JOBS, p, s);
+        match_launch(match_view(b, VO_MP_MAX_JOBS), d_jobs + VO_MP_MAX_JOBS, n_jobs - VO_MP_MAX_JOBS, p, s);
+        return;
+    }
     VO_LAUNCH(k_match_partial, dim3(2048), dim3(256), 0, s, d_jobs, n_jobs, b.partial, b.row_cap, b.n_chunks);
     VO_LAUNCH(k_match_merge, dim3((b.row_cap + 255) / 256, n_jobs), dim3(256), 0, s, d_jobs, (const MatchTop2*)b.partial,
               b.res, b.row_cap, b.n_chunks, p.match_threshold * 0.04f, p.max_ratio);

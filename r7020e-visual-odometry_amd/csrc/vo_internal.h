@@ -179,7 +179,9 @@ struct MatchBuffers {
     int max_jobs = 0, row_cap = 0, n_chunks = 0;
 };
 
-#define VO_MATCH_CHUNK 512           // F2 columns per wave task
+#ifndef VO_MATCH_CHUNK
+#define VO_MATCH_CHUNK 2048          // F2 columns per task (sweep 512/1024/2048 on MI355X)
+#endif
 
 hipError_t match_alloc(MatchBuffers& b, int max_jobs, int row_cap);
 // View whose job slot 0 is slot k0 of b (partial-result rows of jobs k0, k0+1, ...).
