@@ -181,3 +181,22 @@ def test_sequence_pipelined_bit_exact(vo, oracle, syn, seq, calib):
     s2 = ctx.step_batch_dev(dl.data_ptr() + 3 * fs, dr.data_ptr() + 3 * fs, 3)
     _compare_seq(np.concatenate([s1, s2]), ctx.get_landmarks(), routs, rlm)
     ctx.close()
+
+
+def test_sequence_kitti_resolution_bit_exact(vo, oracle, syn):
+    """The whole loop body at KITTI-00's real image size (376 x 1241: odd width, even height),
+    pipelined, equals the oracle's VO.m loop bit for bit."""
+    import torch
+    n = 4
+    L, R, _ = syn.sequence(n, rows=376, cols=1241, step_m=0.5)
+    routs, rlm = oracle.run_sequence(L, R, syn.KITTI00_P0, syn.KITTI00_P1)
+    ctx = vo.Context(376, 1241, 2, calib=vo.calib_from(syn.KITTI00_P0, syn.KITTI00_P1))
+    dl, dr = torch.from_numpy(np.ascontiguousarray(L)).cuda(), torch.from_numpy(np.ascontiguousarray(R)).cuda()
+    torch.cuda.synchronize()
+    fs = L[0].size
+    ctx.step_submit_dev(dl.data_ptr(), dr.data_ptr(), 2)
+    ctx.step_submit_dev(dl.data_ptr() + 2 * fs, dr.data_ptr() + 2 * fs, 2)
+    outs = np.concatenate([ctx.step_collect(), ctx.step_collect()])
+    assert np.all(outs["status"][1:] == 0)
+    _compare_seq(outs, ctx.get_landmarks(), routs, rlm)
+    ctx.close()
