@@ -209,6 +209,14 @@ int vo_step_submit_dev(vo_ctx* ctx, const uint8_t* d_lefts, const uint8_t* d_rig
 int vo_step_collect(vo_ctx* ctx, vo_step_out* outs, int capacity, int* n);
 int vo_steps_pending(const vo_ctx* ctx);
 
+/* Visualisation data of frame `frame` of the most recently collected batch (valid until
+ * that buffer set is reused, i.e. the next-but-one submit): the tracked points'
+ * previous-frame left positions, current left image points and triangulated world points
+ * (remaining_old_features.l_pos / .pos of VO.m:106-116), and every current left detection
+ * (l_pos, VO.m:79).  Any output pointer may be NULL. */
+int vo_fetch_tracks(vo_ctx* ctx, int frame, float* old_l, float* cur_l, double* world, float* det, int capacity,
+                    int* n_tracked, int* n_det);
+
 /* Landmarks accumulated so far ([rows][3] double, world frame). */
 int vo_get_landmarks(vo_ctx* ctx, double* out, int capacity, int* rows);
 /* Reset loop state (features, pose, landmarks). */

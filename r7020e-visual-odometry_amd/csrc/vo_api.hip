@@ -112,6 +112,7 @@ struct vo_ctx {
     struct Pending { int set, B; bool first_tracked; };
     std::deque<Pending> pending;
     int next_step_set = 0;
+    int last_step_set = -1, last_step_B = 0;          // the most recently collected batch (vo_fetch_tracks)
     std::string err;
     Profiler prof;
     int last_B = 0;
@@ -707,6 +708,8 @@ static int collect_batch(vo_ctx* c, vo_step_out* outs, int capacity, int* n_out)
     }
     HIPC(c, hipStreamSynchronize(c->copy_stream));
     c->pending.pop_front();
+    c->last_step_set = P.set;
+    c->last_step_B = B;
     for (int f = 0; f < B; ++f) {
         vo_step_out& o = outs[f];
         memset(&o, 0, sizeof(o));
@@ -796,6 +799,42 @@ int vo_step_collect(vo_ctx* c, vo_step_out* outs, int capacity, int* n)
 
 int vo_steps_pending(const vo_ctx* c) { return c ? (int)c->pending.size() : 0; }
 
+int vo_fetch_tracks(vo_ctx* c, int frame, float* old_l, float* cur_l, double* world, float* det, int capacity,
+                    int* n_tracked, int* n_det)
+{
+    if (!c || capacity < 0) return fail(c, VO_ERR_ARG, "vo_fetch_tracks: bad arguments");
+    if (c->last_step_set < 0 || frame < 0 || frame >= c->last_step_B)
+        return fail(c, VO_ERR_STATE, "vo_fetch_tracks: frame %d not in the last collected batch", frame);
+    hipSetDevice(c->device);
+    SetRef S = set_ref(c, c->last_step_set);
+    const int K = c->sb.kp_cap;
+    int n = 0, nd = 0;
+    HIPC(c, hipMemcpy(&n, S.gb->list_n + 4 * frame + 3, sizeof(int), hipMemcpyDeviceToHost));
+    HIPC(c, hipMemcpy(&nd, S.sb->n_kp + 2 * frame, sizeof(int), hipMemcpyDeviceToHost));
+    n = std::min(std::max(n, 0), K);
+    nd = std::min(std::max(nd, 0), K);
+    if (n_tracked) *n_tracked = n;
+    if (n_det) *n_det = nd;
+    const int m = std::min(n, capacity), md = std::min(nd, capacity);
+    if (m > 0 && (old_l || cur_l || world)) {
+        std::vector<float> op((size_t)m * 4);
+        std::vector<double> ip((size_t)m * 2);
+        HIPC(c, hipMemcpy(op.data(), S.gb->oldpos + (size_t)frame * K * 4, sizeof(float) * 4 * m, hipMemcpyDeviceToHost));
+        HIPC(c, hipMemcpy(ip.data(), S.gb->imgpt + (size_t)frame * K * 2, sizeof(double) * 2 * m, hipMemcpyDeviceToHost));
+        if (world) HIPC(c, hipMemcpy(world, S.gb->world + (size_t)frame * K * 3, sizeof(double) * 3 * m, hipMemcpyDeviceToHost));
+        for (int k = 0; k < m; ++k) {
+            if (old_l) { old_l[2 * k] = op[4 * k]; old_l[2 * k + 1] = op[4 * k + 1]; }
+            if (cur_l) { cur_l[2 * k] = (float)ip[2 * k]; cur_l[2 * k + 1] = (float)ip[2 * k + 1]; }
+        }
+    }
+    if (det && md > 0) {
+        std::vector<vo_keypoint> kp(md);
+        HIPC(c, hipMemcpy(kp.data(), S.sb->kp + (size_t)(2 * frame) * K, sizeof(vo_keypoint) * md, hipMemcpyDeviceToHost));
+        for (int k = 0; k < md; ++k) { det[2 * k] = kp[k].x; det[2 * k + 1] = kp[k].y; }
+    }
+    return VO_OK;
+}
+
 int vo_get_landmarks(vo_ctx* c, double* out, int capacity, int* rows)
 {
     if (!c) return VO_ERR_ARG;
@@ -812,6 +851,7 @@ int vo_reset(vo_ctx* c)
     HIPC(c, hipDeviceSynchronize());                   // drops any pending asynchronous batches
     c->pending.clear();
     c->next_step_set = 0;
+    c->last_step_set = -1;
     c->have_features = false;
     c->frame_index = 0;
     memcpy(c->pose, I4, sizeof(I4));

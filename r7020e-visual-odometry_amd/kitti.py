@@ -201,32 +201,39 @@ class KittiSequence:
         self._pool.shutdown(wait=True)
 
 
-def _pipelined(ctx, batches, dev) -> list:
+def _pipelined(ctx, batches, dev, on_collect=None) -> list:
     """Drive the loop body through vo_step_submit_dev / vo_step_collect: while batch n's
     kernels run, the host decodes and uploads batch n+1 (threaded PNG decode, pinned H2D),
     and batch n+1's SIFT overlaps batch n's geometry.  Input tensors stay referenced until
     their batch is collected."""
     import torch
     outs, inflight = [], []
-    for _b0, L, R in batches:
+
+    def collect():
+        outs.append(ctx.step_collect())
+        b0, L = inflight.pop(0)[2:]
+        if on_collect is not None:
+            on_collect(b0, L, outs)
+    for b0, L, R in batches:
         dl = torch.from_numpy(L).pin_memory().to(dev, non_blocking=True)
         dr = torch.from_numpy(R).pin_memory().to(dev, non_blocking=True)
         torch.cuda.current_stream(dev).synchronize()         # inputs ready before the submit
         ctx.step_submit_dev(dl.data_ptr(), dr.data_ptr(), L.shape[0])
-        inflight.append((dl, dr))
+        inflight.append((dl, dr, b0, L if on_collect is not None else None))
         if ctx.steps_pending() == 2:
-            outs.append(ctx.step_collect())
-            inflight.pop(0)
+            collect()
     while ctx.steps_pending():
-        outs.append(ctx.step_collect())
-        inflight.pop(0)
+        collect()
     return outs
 
 
-def run(seq: KittiSequence, batch: int = 16, stop: int | None = None, device: int = 0, ctx=None):
+def run(seq: KittiSequence, batch: int = 16, stop: int | None = None, device: int = 0, ctx=None,
+        viz_dir: str | os.PathLike | None = None, viz_every: int = 100):
     """The VO.m loop over a KITTI sequence through libvo: frames in batches of `batch`
     (pipelined vo_step_submit_dev / vo_step_collect, tracking carried across batches), H2D
-    from pinned host buffers.
+    from pinned host buffers.  With `viz_dir`, every `viz_every`-th frame writes the reference's
+    figures (`viz.snapshot`: img/<i>/view.png, map.svg, error.svg, 3d_map.svg; the landmark map
+    in them includes the whole batch of frame i).
     Returns (poses [n, 4, 4] with frame 0 = identity, per-frame vo_step_out records,
     landmarks [L, 3])."""
     import torch
@@ -234,7 +241,18 @@ def run(seq: KittiSequence, batch: int = 16, stop: int | None = None, device: in
     own = ctx is None
     if own:
         ctx = vo.Context(seq.rows, seq.cols, batch, device=device, calib=vo.calib_from(seq.P1, seq.P2))
-    outs = _pipelined(ctx, seq.batches(batch, 0, stop), torch.device("cuda", device))
+    hook = None
+    if viz_dir is not None:
+        from . import viz
+
+        def hook(b0, L, done):                               # VO.m:168-199 every viz_every-th frame
+            poses = np.stack([o["pose"] for o in np.concatenate(done)])
+            for f in range(L.shape[0]):
+                i = b0 + f
+                if i > 0 and i % viz_every == 0:
+                    viz.snapshot(viz_dir, i, L[f], ctx.fetch_tracks(f), poses[: i + 1], seq.gt, seq.times,
+                                 ctx.get_landmarks())
+    outs = _pipelined(ctx, seq.batches(batch, 0, stop), torch.device("cuda", device), hook)
     outs = np.concatenate(outs) if outs else np.zeros(0, vo.STEP_DTYPE)
     poses = np.stack([o["pose"] for o in outs]) if len(outs) else np.zeros((0, 4, 4))
     lm = ctx.get_landmarks()

@@ -88,7 +88,7 @@ EXPORTS = [
     "vo_default_sift_params", "vo_default_match_params", "vo_default_ransac_params", "vo_create", "vo_destroy",
     "vo_set_calib", "vo_last_error", "vo_sift", "vo_match", "vo_track", "vo_triangulate", "vo_estworldpose",
     "vo_landmarks", "vo_step", "vo_step_batch", "vo_step_batch_dev", "vo_step_submit_dev", "vo_step_collect",
-    "vo_steps_pending", "vo_get_landmarks", "vo_reset",
+    "vo_steps_pending", "vo_fetch_tracks", "vo_get_landmarks", "vo_reset",
     "vo_sift_match_batch_dev", "vo_fetch_keypoints", "vo_fetch_stereo_pairs", "vo_stream", "vo_set_profiling",
     "vo_kernel_times", "vo_set_frame_index", "vo_set_concurrency",
 ]
@@ -140,6 +140,8 @@ def load_library(path: str | os.PathLike | None = None):
     L.vo_step_submit_dev.argtypes = [vp, vp, vp, C.c_int]
     L.vo_step_collect.argtypes = [vp, P(StepOut), C.c_int, P(C.c_int)]
     L.vo_steps_pending.argtypes = [vp]
+    L.vo_fetch_tracks.argtypes = [vp, C.c_int, P(C.c_float), P(C.c_float), P(C.c_double), P(C.c_float), C.c_int,
+                                  P(C.c_int), P(C.c_int)]
     L.vo_get_landmarks.argtypes = [vp, P(C.c_double), C.c_int, P(C.c_int)]
     L.vo_reset.argtypes = [vp]
     L.vo_set_frame_index.argtypes = [vp, C.c_long]
@@ -350,6 +352,21 @@ class Context:
 
     def steps_pending(self) -> int:
         return int(self.lib.vo_steps_pending(self.h))
+
+    def fetch_tracks(self, frame: int) -> dict:
+        """Visualisation data of `frame` of the last collected batch (vo_fetch_tracks):
+        old_l / cur_l [K, 2] (1-based), world [K, 3], det [N, 2] (all current left detections)."""
+        nt, nd = C.c_int(0), C.c_int(0)
+        self._check(self.lib.vo_fetch_tracks(self.h, frame, None, None, None, None, 0, C.byref(nt), C.byref(nd)))
+        cap = max(nt.value, nd.value, 1)
+        old = np.zeros((cap, 2), np.float32)
+        cur = np.zeros((cap, 2), np.float32)
+        world = np.zeros((cap, 3))
+        det = np.zeros((cap, 2), np.float32)
+        self._check(self.lib.vo_fetch_tracks(self.h, frame, _p(old, C.c_float), _p(cur, C.c_float), _p(world, C.c_double),
+                                             _p(det, C.c_float), cap, C.byref(nt), C.byref(nd)))
+        k, n = nt.value, nd.value
+        return {"old_l": old[:k].copy(), "cur_l": cur[:k].copy(), "world": world[:k].copy(), "det": det[:n].copy()}
 
     def step(self, left: np.ndarray, right: np.ndarray):
         return self.step_batch(left[None], right[None])[0]

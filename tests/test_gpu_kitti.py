@@ -48,3 +48,27 @@ def test_sharded_blocks_chain_to_single_run(vo, syn, tmp_path):
         assert rel.shape == (n, 4, 4)
         assert np.array_equal(sharding.chain(rel), poses), world
     seq.close()
+
+
+def test_kitti_driver_visualisation(vo, syn, tmp_path):
+    """viz_every frames write the reference's figure set (VO.m:168-199); fetch_tracks returns
+    exactly n_tracked tracked points and n_left detections of that frame."""
+    import vo_amd  # noqa: F401
+    from r7020e_visual_odometry_amd import kitti, viz
+    from test_kitti import write_kitti_layout
+    n = 8
+    L, R, _gt = syn.sequence(n, step_m=0.5)
+    write_kitti_layout(tmp_path, L, R)
+    seq = kitti.KittiSequence(tmp_path, "00")
+    P1, P2 = syn.calib()
+    ctx = vo.Context(375, 1242, 4, calib=vo.calib_from(P1, P2))
+    poses, outs, lm = kitti.run(seq, batch=4, ctx=ctx, viz_dir=tmp_path / "out", viz_every=3)
+    for i in (3, 6):
+        d = tmp_path / "out" / "img" / str(i)
+        assert (d / "view.png").exists() and (d / "3d_map.svg").exists()
+        assert viz.read_png_rgb(d / "view.png").shape == (375, 1242, 3)
+    tr = ctx.fetch_tracks(3)                             # frame 7 of the sequence (last batch)
+    assert len(tr["cur_l"]) == outs[7]["n_tracked"] and len(tr["det"]) == outs[7]["n_left"]
+    assert np.all(np.isfinite(tr["world"]))
+    seq.close()
+    ctx.close()
