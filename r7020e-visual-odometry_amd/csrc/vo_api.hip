@@ -848,7 +848,10 @@ int vo_reset(vo_ctx* c)
 {
     if (!c) return VO_ERR_ARG;
     hipSetDevice(c->device);
-    HIPC(c, hipDeviceSynchronize());                   // drops any pending asynchronous batches
+    // drops any pending asynchronous batches: wait for this context's streams only
+    HIPC(c, hipStreamSynchronize(c->stream));
+    for (int k = 0; k < vo_ctx::MAX_SUB; ++k) HIPC(c, hipStreamSynchronize(c->sub[k]));
+    HIPC(c, hipStreamSynchronize(c->copy_stream));
     c->pending.clear();
     c->next_step_set = 0;
     c->last_step_set = -1;
