@@ -774,26 +774,17 @@ __device__ __forceinline__ void decode_word(const Pyramid* __restrict__ py, int 
 // ---------------------------------------------------------------------------
 // 26-neighbour extremum test, streaming.  One wave per (image, octave, strip
 // of 128 columns, band of VO_EXT_BAND interior rows); lane l owns columns
-// xs+2l, xs+2l+1.  The wave walks the band's rows (+1 above and below): per
-// row it loads the L+3 Gaussian levels (8-B loads + one halo column each
-// side), forms D_l = G_{l+1} - G_l (never stored), reduces each level to its
+// xs+l and xs+64+l, so a ballot over the lanes is a whole 64-column mask word (no
+// bit interleaving on the scalar unit).  The wave walks the band's rows (+1 above
+// and below): per row it loads the L+3 Gaussian levels (two coalesced 4-B loads +
+// one halo column: xs-1 in lane 0, xs+128 in lane 63), forms D_l = G_{l+1} - G_l
+// (never stored), reduces each level to its
 // horizontal 3-max/3-min (neighbours by lane shuffle), and keeps the last 3
 // rows of those in a register window (rows unrolled by 3, static slots).
 // Row t-1 is then tested: val >= max of its 3x3x3 block (val included)
-// <=> val >= all 26 neighbours.  Two ballots per (row, layer) are interleaved
-// into the two 64-column mask words of the strip.  Input rows are prefetched
-// 3 rows ahead.
+// <=> val >= all 26 neighbours.  The two ballots per (row, layer) are the two
+// 64-column mask words of the strip.  Input rows are prefetched 3 rows ahead.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t vo_spread32(uint64_t x)     // bit i -> bit 2i
-{
-    x &= 0xffffffffull;
-    x = (x | (x << 16)) & 0x0000ffff0000ffffull;
-    x = (x | (x << 8)) & 0x00ff00ff00ff00ffull;
-    x = (x | (x << 4)) & 0x0f0f0f0f0f0f0f0full;
-    x = (x | (x << 2)) & 0x3333333333333333ull;
-    x = (x | (x << 1)) & 0x5555555555555555ull;
-    return x;
-}
 
 template <int L>
 __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ py, const float* __restrict__ arena,
@@ -816,20 +807,20 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
     const int ir = rows - 2 * VO_SIFT_BORDER;
     const int r0 = VO_SIFT_BORDER + band * VO_EXT_BAND;                 // first tested row
     const int nrow = min(VO_EXT_BAND, ir - band * VO_EXT_BAND);          // tested rows in this band
-    const int xs = strip * 128, xc = xs + 2 * lane;
-    // halo columns: lane 0 -> xs-1, lane 1 -> xs+128 (others reload lane 0's)
-    const int hx = lane == 1 ? xs + 128 : max(xs - 1, 0);
+    const int xs = strip * 128, xa = xs + lane, xb = xa + 64;
+    // halo columns: lane 63 -> xs+128, the others xs-1 (used by lane 0; same cache line)
+    const int hx = lane == 63 ? xs + 128 : max(xs - 1, 0);
     const float* base = arena + img * py->istride;
     size_t goff[NG];
 #pragma unroll
     for (int lv = 0; lv < NG; ++lv) goff[lv] = g.g_off[lv];
     const int wr = py->wrow[o];
     unsigned long long* mrow = mask + (size_t)img * py->n_words;
-    const bool in0 = xc >= VO_SIFT_BORDER && xc < cols - VO_SIFT_BORDER;
-    const bool in1 = xc + 1 >= VO_SIFT_BORDER && xc + 1 < cols - VO_SIFT_BORDER;
+    const bool in0 = xa >= VO_SIFT_BORDER && xa < cols - VO_SIFT_BORDER;
+    const bool in1 = xb >= VO_SIFT_BORDER && xb < cols - VO_SIFT_BORDER;
 
     typedef float f2_t __attribute__((ext_vector_type(2)));
-    f2_t pm[W][NG];                                  // prefetched main columns, per window slot
+    f2_t pm[W][NG];                                  // prefetched columns {xa, xb}, per window slot
     float ph[W][NG];                                 // prefetched halo column
     f2_t hmx[W][ND], hmn[W][ND];                     // horizontal 3-max / 3-min per row slot
     f2_t dc[W][L];                                   // D of layers 1..L per row slot (centres)
@@ -839,7 +830,7 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
         const int y_ = min(r0 - 1 + (T), rows - 1);                                                \
         const float* rp_ = base + (size_t)y_ * pitch;                                              \
         _Pragma("unroll") for (int lv = 0; lv < NG; ++lv) {                                        \
-            pm[SL][lv] = *reinterpret_cast<const f2_t*>(rp_ + goff[lv] + xc);                      \
+            pm[SL][lv] = f2_t{rp_[goff[lv] + xa], rp_[goff[lv] + xb]};                             \
             ph[SL][lv] = rp_[goff[lv] + hx];                                                       \
         }                                                                                          \
     } while (0)
@@ -857,14 +848,15 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
         VO_ET_LOAD(t + W, SL);                        // refill the slot with row t+3
 #pragma unroll
         for (int lv = 0; lv < ND; ++lv) {
-            float left = __shfl_up(d[lv].y, 1);
-            float right = __shfl_down(d[lv].x, 1);
-            const float hr = __shfl(hd[lv], 1);
-            if (lane == 0) left = hd[lv];
-            if (lane == 63) right = hr;
-            const float m01 = fmaxf(d[lv].x, d[lv].y), n01 = fminf(d[lv].x, d[lv].y);
-            hmx[SL][lv] = f2_t{fmaxf(left, m01), fmaxf(m01, right)};
-            hmn[SL][lv] = f2_t{fminf(left, n01), fminf(n01, right)};
+            // neighbours of xa: xa-1 (lane 0: halo xs-1), xa+1 (lane 63: xs+64 = lane 0's xb);
+            // of xb: xb-1 (lane 0: xs+63 = lane 63's xa), xb+1 (lane 63: halo xs+128)
+            float la = __shfl_up(d[lv].x, 1), ra = __shfl_down(d[lv].x, 1);
+            float lb = __shfl_up(d[lv].y, 1), rb = __shfl_down(d[lv].y, 1);
+            const float b0 = __shfl(d[lv].y, 0), a63 = __shfl(d[lv].x, 63);
+            if (lane == 0) { la = hd[lv]; lb = a63; }
+            if (lane == 63) { ra = b0; rb = hd[lv]; }
+            hmx[SL][lv] = f2_t{fmaxf(fmaxf(la, d[lv].x), ra), fmaxf(fmaxf(lb, d[lv].y), rb)};
+            hmn[SL][lv] = f2_t{fminf(fminf(la, d[lv].x), ra), fminf(fminf(lb, d[lv].y), rb)};
         }
 #pragma unroll
         for (int l = 0; l < L; ++l) dc[SL][l] = d[l + 1];
@@ -891,9 +883,7 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
                                             c ? mn3[layer + 1].y : mn3[layer + 1].x);
                     e[c] = fabsf(val) > thr && ((val > 0 && val >= bmx) || (!(val > 0) && val <= bmn));
                 }
-                const uint64_t b0 = __ballot(e[0] && in0), b1 = __ballot(e[1] && in1);
-                const uint64_t w0 = vo_spread32(b0) | (vo_spread32(b1) << 1);
-                const uint64_t w1 = vo_spread32(b0 >> 32) | (vo_spread32(b1 >> 32) << 1);
+                const uint64_t w0 = __ballot(e[0] && in0), w1 = __ballot(e[1] && in1);
                 const int k = 2 * strip + lane;
                 if (lane < 2 && k < wr && t - 2 < nrow)
                     mrow[py->wbase[o * L + layer - 1] + (size_t)(r - VO_SIFT_BORDER) * wr + k] = lane ? w1 : w0;
@@ -1720,6 +1710,14 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
     }
 }
 
+// grid of the wave-per-keypoint kernels (grid-stride over the flat keypoint space)
+static int feature_grid(const char* env)
+{
+    const char* v = getenv(env);
+    const int g = v ? atoi(v) : 8192;
+    return g > 0 ? g : 8192;
+}
+
 void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
                            const Pyramid* d_py)
 {
@@ -1730,11 +1728,11 @@ void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const v
     VO_LAUNCH(k_seg_emit, gs, dim3(256), 0, s, d_py, b.mask, (const uint32_t*)b.woff, b.cand, b.cand_cap);
     VO_LAUNCH(k_refine, dim3(512), dim3(256), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.cand_cap, n_img,
               p.contrast_threshold, p.edge_threshold, p.sigma);
-    VO_LAUNCH(k_orient, dim3(8192), dim3(64), 0, s, d_py, A, b.n_cand, b.cout, b.cand_cap, n_img);
+    VO_LAUNCH(k_orient, dim3(feature_grid("VO_ORIENT_GRID")), dim3(64), 0, s, d_py, A, b.n_cand, b.cout, b.cand_cap, n_img);
     VO_LAUNCH(k_scan_cands, dim3(n_img), dim3(1024), 0, s, b.cout, b.n_cand, b.koff, b.n_kp, b.cand_cap);
     VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, b.n_cand, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
                        n_img, p.upsample);
-    VO_LAUNCH(k_desc, dim3(8192), dim3(64), 0, s, d_py, A, b.kpi, b.n_kp, b.desc, b.meta, b.kp_cap, n_img);
+    VO_LAUNCH(k_desc, dim3(feature_grid("VO_DESC_GRID")), dim3(64), 0, s, d_py, A, b.kpi, b.n_kp, b.desc, b.meta, b.kp_cap, n_img);
 }
 
 void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img, const vo_sift_params& p,

@@ -229,7 +229,13 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bail("stream", e);
     for (int k = 0; k < vo_ctx::MAX_SUB; ++k) {
-        if ((e = hipStreamCreateWithFlags(&c->sub[k], hipStreamNonBlocking)) != hipSuccess) return bail("stream", e);
+        // sub[0] carries the scale space (the HBM-bound critical path): optionally at the
+        // highest stream priority so its workgroups are dispatched ahead of the feature stream's
+        static const int ss_prio = getenv("VO_SS_PRIO") ? atoi(getenv("VO_SS_PRIO")) : 0;
+        int lo_p = 0, hi_p = 0;
+        hipDeviceGetStreamPriorityRange(&lo_p, &hi_p);
+        const int prio = (k == 0 && ss_prio > 0) ? hi_p : (k == 1 && ss_prio < 0) ? hi_p : lo_p;
+        if ((e = hipStreamCreateWithPriority(&c->sub[k], hipStreamNonBlocking, prio)) != hipSuccess) return bail("stream", e);
         if ((e = hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
     }
     if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("event", e);
