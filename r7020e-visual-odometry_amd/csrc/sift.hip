@@ -786,6 +786,17 @@ __device__ __forceinline__ void decode_word(const Pyramid* __restrict__ py, int 
 // 64-column mask words of the strip.  Input rows are prefetched 3 rows ahead.
 // ---------------------------------------------------------------------------
 
+// whole-wave lane shifts on the VALU (GFX9 DPP wave_shr:1 / wave_shl:1) instead of
+// LDS-routed ds_bpermute shuffles; the lane without a source keeps its own value
+__device__ __forceinline__ float vo_wave_shr1(float x)      // lane i <- lane i-1
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float vo_wave_shl1(float x)      // lane i <- lane i+1
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), 0x130, 0xf, 0xf, false));
+}
+
 template <int L>
 __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                                    unsigned long long* __restrict__ mask, float thr, int n_img)
@@ -816,6 +827,9 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
     for (int lv = 0; lv < NG; ++lv) goff[lv] = g.g_off[lv];
     const int wr = py->wrow[o];
     unsigned long long* mrow = mask + (size_t)img * py->n_words;
+    int wb[L];                                       // mask word base per layer, hoisted: the mask
+#pragma unroll                                       // stores could alias *py for the compiler
+    for (int l = 0; l < L; ++l) wb[l] = py->wbase[o * L + l];
     const bool in0 = xa >= VO_SIFT_BORDER && xa < cols - VO_SIFT_BORDER;
     const bool in1 = xb >= VO_SIFT_BORDER && xb < cols - VO_SIFT_BORDER;
 
@@ -850,9 +864,10 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
         for (int lv = 0; lv < ND; ++lv) {
             // neighbours of xa: xa-1 (lane 0: halo xs-1), xa+1 (lane 63: xs+64 = lane 0's xb);
             // of xb: xb-1 (lane 0: xs+63 = lane 63's xa), xb+1 (lane 63: halo xs+128)
-            float la = __shfl_up(d[lv].x, 1), ra = __shfl_down(d[lv].x, 1);
-            float lb = __shfl_up(d[lv].y, 1), rb = __shfl_down(d[lv].y, 1);
-            const float b0 = __shfl(d[lv].y, 0), a63 = __shfl(d[lv].x, 63);
+            float la = vo_wave_shr1(d[lv].x), ra = vo_wave_shl1(d[lv].x);
+            float lb = vo_wave_shr1(d[lv].y), rb = vo_wave_shl1(d[lv].y);
+            const float b0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d[lv].y), 0));
+            const float a63 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d[lv].x), 63));
             if (lane == 0) { la = hd[lv]; lb = a63; }
             if (lane == 63) { ra = b0; rb = hd[lv]; }
             hmx[SL][lv] = f2_t{fmaxf(fmaxf(la, d[lv].x), ra), fmaxf(fmaxf(lb, d[lv].y), rb)};
@@ -881,12 +896,15 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
                                             c ? mx3[layer + 1].y : mx3[layer + 1].x);
                     const float bmn = fminf(fminf(c ? mn3[layer - 1].y : mn3[layer - 1].x, c ? mn3[layer].y : mn3[layer].x),
                                             c ? mn3[layer + 1].y : mn3[layer + 1].x);
-                    e[c] = fabsf(val) > thr && ((val > 0 && val >= bmx) || (!(val > 0) && val <= bmn));
+                    // branch-free form of |val| > thr && (val > 0 ? val >= bmx : val <= bmn):
+                    // negation by the sign select is exact
+                    const float sg = val > 0 ? 1.0f : -1.0f, ref = val > 0 ? bmx : bmn;
+                    e[c] = (fabsf(val) > thr) & (sg * val >= sg * ref);
                 }
                 const uint64_t w0 = __ballot(e[0] && in0), w1 = __ballot(e[1] && in1);
                 const int k = 2 * strip + lane;
                 if (lane < 2 && k < wr && t - 2 < nrow)
-                    mrow[py->wbase[o * L + layer - 1] + (size_t)(r - VO_SIFT_BORDER) * wr + k] = lane ? w1 : w0;
+                    mrow[wb[layer - 1] + (size_t)(r - VO_SIFT_BORDER) * wr + k] = lane ? w1 : w0;
             }
         }
     };
@@ -1436,8 +1454,9 @@ __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, con
         for (int s0 = lane; s0 < nsamp; s0 += 64 * U) {
             float crot[U], rrot[U], gdx[U], gdy[U];
             bool ok[U];
+            uint32_t off[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {                // phase 1: indices and gradient loads (every listed sample is valid)
+            for (int u = 0; u < U; ++u) {                // phase 1a: rows (LDS walk) and offsets of all U samples
                 const int s = s0 + 64 * u;
                 ok[u] = s < nsamp;
                 const int sc = ok[u] ? s : nsamp - 1;
@@ -1445,9 +1464,19 @@ __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, con
                 const int i = lo - radius, j = rlo[lo] + (sc - rstart[lo]);
                 crot[u] = (float)j * cos_t - (float)i * sin_t;
                 rrot[u] = (float)j * sin_t + (float)i * cos_t;
-                const uint32_t o = (uint32_t)((pyy + i) * P + px + j);   // 32-bit offset from the uniform base
-                gdx[u] = gim[o + 1] - gim[o - 1];
-                gdy[u] = gim[o - P] - gim[o + P];
+                off[u] = (uint32_t)((pyy + i) * P + px + j);   // 32-bit offset from the uniform base
+            }
+            float g4[U][4];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {                // phase 1b: all 4U gradient loads in flight together
+                const uint32_t o = off[u];                // (every listed sample is valid)
+                g4[u][0] = gim[o + 1]; g4[u][1] = gim[o - 1];
+                g4[u][2] = gim[o - P]; g4[u][3] = gim[o + P];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                gdx[u] = g4[u][0] - g4[u][1];
+                gdy[u] = g4[u][2] - g4[u][3];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {                // phase 2: weights, bins, fixed-point LDS atomics
