@@ -241,6 +241,11 @@ int vo_sift_match_batch_dev(vo_ctx* ctx, const uint8_t* d_lefts, const uint8_t* 
  * a frame.  Host output buffers. */
 int vo_fetch_keypoints(vo_ctx* ctx, int image, vo_keypoint* kps, uint8_t* desc, int capacity, int* n);
 int vo_fetch_stereo_pairs(vo_ctx* ctx, int frame, uint32_t* pairs, int capacity, int* n);
+/* Gaussian scale-space level G(octave, level) of image i from the last batched
+ * call (rows x cols floats, tightly packed; out == NULL only reports the size).
+ * Diagnostic: the scale space has no MATLAB counterpart (detectSIFTFeatures
+ * keeps it internal, VO.m:79-80); parity tests compare it with the oracle. */
+int vo_fetch_gaussian(vo_ctx* ctx, int image, int octave, int level, float* out, int capacity, int* rows, int* cols);
 
 /* HIP stream the context launches on (hipStream_t as void*), and per-kernel
  * timing over the last call (for bench.py's roofline; ms). */

@@ -561,6 +561,26 @@ int vo_fetch_keypoints(vo_ctx* c, int image, vo_keypoint* kps, uint8_t* desc, in
     return VO_OK;
 }
 
+int vo_fetch_gaussian(vo_ctx* c, int image, int octave, int level, float* out, int capacity, int* rows, int* cols)
+{
+    if (!c || image < 0 || image >= c->sb.n_img || octave < 0 || octave >= c->py.n_oct || level < 0 ||
+        level >= c->py.L + 3)
+        return fail(c, VO_ERR_ARG, "vo_fetch_gaussian: bad image/octave/level");
+    hipSetDevice(c->device);
+    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipEventSynchronize(c->ev_done[c->last_set]));
+    const SiftBuffers& B = (c->last_set == 1 && image < 2 * c->max_batch) ? c->aux.sb : c->sb;
+    const OctGeom& g = c->py.oct[octave];
+    if (rows) *rows = g.rows;
+    if (cols) *cols = g.cols;
+    if (!out) return VO_OK;
+    if (capacity < g.rows * g.cols) return fail(c, VO_ERR_CAPACITY, "vo_fetch_gaussian: capacity %d < %d", capacity, g.rows * g.cols);
+    const float* src = B.arena + (size_t)image * c->py.istride + g.g_off[level];
+    HIPC(c, hipMemcpy2D(out, sizeof(float) * g.cols, src, sizeof(float) * g.pitch, sizeof(float) * g.cols, g.rows,
+                        hipMemcpyDeviceToHost));
+    return VO_OK;
+}
+
 int vo_fetch_stereo_pairs(vo_ctx* c, int frame, uint32_t* pairs, int capacity, int* n)
 {
     if (!c || frame < 0 || frame >= c->max_batch) return fail(c, VO_ERR_ARG, "vo_fetch_stereo_pairs: bad frame");

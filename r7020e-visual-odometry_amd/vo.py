@@ -89,7 +89,7 @@ EXPORTS = [
     "vo_set_calib", "vo_last_error", "vo_sift", "vo_match", "vo_track", "vo_triangulate", "vo_estworldpose",
     "vo_landmarks", "vo_step", "vo_step_batch", "vo_step_batch_dev", "vo_step_submit_dev", "vo_step_collect",
     "vo_steps_pending", "vo_fetch_tracks", "vo_get_landmarks", "vo_reset",
-    "vo_sift_match_batch_dev", "vo_fetch_keypoints", "vo_fetch_stereo_pairs", "vo_stream", "vo_set_profiling",
+    "vo_sift_match_batch_dev", "vo_fetch_keypoints", "vo_fetch_stereo_pairs", "vo_fetch_gaussian", "vo_stream", "vo_set_profiling",
     "vo_kernel_times", "vo_set_frame_index", "vo_set_concurrency",
 ]
 
@@ -148,6 +148,7 @@ def load_library(path: str | os.PathLike | None = None):
     L.vo_sift_match_batch_dev.argtypes = [vp, vp, vp, C.c_int, P(PairStats)]
     L.vo_fetch_keypoints.argtypes = [vp, C.c_int, P(Keypoint), P(C.c_uint8), C.c_int, P(C.c_int)]
     L.vo_fetch_stereo_pairs.argtypes = [vp, C.c_int, P(C.c_uint32), C.c_int, P(C.c_int)]
+    L.vo_fetch_gaussian.argtypes = [vp, C.c_int, C.c_int, C.c_int, P(C.c_float), C.c_int, P(C.c_int), P(C.c_int)]
     L.vo_stream.argtypes = [vp]
     L.vo_stream.restype = vp
     L.vo_set_profiling.argtypes = [vp, C.c_int]
@@ -267,6 +268,14 @@ class Context:
         n = C.c_int(0)
         self._check(self.lib.vo_fetch_stereo_pairs(self.h, frame, _p(pairs, C.c_uint32), cap, C.byref(n)))
         return pairs[: min(n.value, cap)].copy()
+
+    def fetch_gaussian(self, image: int, octave: int, level: int) -> np.ndarray:
+        """Gaussian level G(octave, level) of image `image` of the last batched call (diagnostic)."""
+        r, c = C.c_int(0), C.c_int(0)
+        self._check(self.lib.vo_fetch_gaussian(self.h, image, octave, level, None, 0, C.byref(r), C.byref(c)))
+        out = np.empty((r.value, c.value), np.float32)
+        self._check(self.lib.vo_fetch_gaussian(self.h, image, octave, level, _p(out, C.c_float), out.size, None, None))
+        return out
 
     # ---- find_remaining_points ----
     def track(self, old_l, old_r, cur_l, cur_r) -> np.ndarray:
