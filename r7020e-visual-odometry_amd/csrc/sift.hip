@@ -1186,11 +1186,14 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
 // per lane per iteration with every gradient load issued first.  Smoothing,
 // peak test and interpolation as the oracle.  (A lane's u32 partial of one bin
 // holds < 11k samples' weights: windows up to ~7e5 samples.)
+template <int HS>
 __global__ __launch_bounds__(64) void k_orient(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                                const int* __restrict__ n_cand, CandOut* __restrict__ cout,
                                                int cand_cap, int n_img)
 {
-    constexpr int HS = 40;                                // per-lane histogram stride (16-B rows)
+    // HS: per-lane histogram stride.  Odd (37): lanes adding to the same bin hit distinct
+    // banks; 40 (= 8 mod 64 banks) put every 8th lane on one bank (k_orient ~2 % slower).
+    static_assert(HS >= VO_SIFT_ORI_BINS && (HS * 64) % 4 == 0, "per-lane rows hold the 36 bins");
     __shared__ __attribute__((aligned(16))) uint32_t hp[HS * 64];
     __shared__ float tf[VO_SIFT_ORI_BINS];
     __shared__ float hs[VO_SIFT_ORI_BINS];
@@ -1214,7 +1217,8 @@ __global__ __launch_bounds__(64) void k_orient(const Pyramid* __restrict__ py, c
         const float expf_scale = -1.0f / (2.0f * sigw * sigw);
         typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int b2 = 0; b2 < HS; b2 += 4) *reinterpret_cast<u4_t*>(&hp[lane * HS + b2]) = u4_t{0u, 0u, 0u, 0u};
+        for (int b2 = 4 * lane; b2 < HS * 64; b2 += 256) *reinterpret_cast<u4_t*>(&hp[b2]) = u4_t{0u, 0u, 0u, 0u};
+        __syncthreads();
         const int side = 2 * radius + 1, nsamp = side * side;
         const float inv_side = 1.0f / (float)side;          // (s + 0.5) * inv_side is exact enough to floor (s < 2^22)
         constexpr int U = 4;
@@ -1359,8 +1363,7 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
 // (same cell, often the same orientation bin) no longer serialise on one LDS address.
 // Copy stride 360 dwords = 8 mod 32 banks.  u32 fixed point (vo_desc_fx_quant) sums
 // are order-free, so the copies are folded after the loop without changing a bit.
-#define DCOPIES 4
-
+template <int DCOPIES>
 __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                              const KpInt* __restrict__ kpi, const int* __restrict__ n_kp,
                                              uint8_t* __restrict__ desc, DescMeta* __restrict__ meta, int kp_cap, int n_img)
@@ -1469,9 +1472,9 @@ __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, con
             float g4[U][4];
 #pragma unroll
             for (int u = 0; u < U; ++u) {                // phase 1b: all 4U gradient loads in flight together
-                const uint32_t o = off[u];                // (every listed sample is valid)
-                g4[u][0] = gim[o + 1]; g4[u][1] = gim[o - 1];
-                g4[u][2] = gim[o - P]; g4[u][3] = gim[o + P];
+                const float* gp = gim + off[u];           // (every listed sample is valid); +-1 as immediate offsets
+                g4[u][0] = gp[1]; g4[u][1] = gp[-1];
+                g4[u][2] = gp[-(ptrdiff_t)P]; g4[u][3] = gp[P];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -1582,9 +1585,9 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
     static const int use_pipe = getenv("VO_BLUR_PIPE") ? atoi(getenv("VO_BLUR_PIPE")) : 0;
     if constexpr (MODE == 0 && RAD > 0) if (!use_pipe) {
         static const int th_env = getenv("VO_BLUR_TH") ? atoi(getenv("VO_BLUR_TH")) : 128;
-        static const int wave_target = getenv("VO_BLUR_WAVES") ? atoi(getenv("VO_BLUR_WAVES")) : 1024;
+        static const int wave_target = getenv("VO_BLUR_WAVES") ? atoi(getenv("VO_BLUR_WAVES")) : 2048;
         // band height: a multiple of P, at most th_env, lowered on small octaves until
-        // the launch has ~wave_target waves (8 per CU) -- small planes are latency-bound
+        // the launch has ~wave_target waves (2048: 8 per CU; 1024 measured ~1.5 % slower) -- small planes are latency-bound
         // level blurs of planes at most cpl2_maxc wide use 2 columns per lane (128-column
         // strips, half the ring registers): more waves and fewer idle lanes at the
         // narrow octaves, where the kernel is latency-bound rather than HBM-bound
@@ -1757,11 +1760,14 @@ void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const v
     VO_LAUNCH(k_seg_emit, gs, dim3(256), 0, s, d_py, b.mask, (const uint32_t*)b.woff, b.cand, b.cand_cap);
     VO_LAUNCH(k_refine, dim3(512), dim3(256), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.cand_cap, n_img,
               p.contrast_threshold, p.edge_threshold, p.sigma);
-    VO_LAUNCH(k_orient, dim3(feature_grid("VO_ORIENT_GRID")), dim3(64), 0, s, d_py, A, b.n_cand, b.cout, b.cand_cap, n_img);
+    VO_LAUNCH_NAMED("k_orient", (k_orient<37>), dim3(feature_grid("VO_ORIENT_GRID")), dim3(64), 0, s, d_py, A, b.n_cand,
+                    b.cout, b.cand_cap, n_img);
     VO_LAUNCH(k_scan_cands, dim3(n_img), dim3(1024), 0, s, b.cout, b.n_cand, b.koff, b.n_kp, b.cand_cap);
     VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, b.n_cand, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
                        n_img, p.upsample);
-    VO_LAUNCH(k_desc, dim3(feature_grid("VO_DESC_GRID")), dim3(64), 0, s, d_py, A, b.kpi, b.n_kp, b.desc, b.meta, b.kp_cap, n_img);
+    // 4 histogram copies: 2 -> +4 %, 8 -> +33 % k_desc time (MI355X)
+    VO_LAUNCH_NAMED("k_desc", (k_desc<4>), dim3(feature_grid("VO_DESC_GRID")), dim3(64), 0, s, d_py, A, b.kpi, b.n_kp, b.desc,
+                    b.meta, b.kp_cap, n_img);
 }
 
 void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img, const vo_sift_params& p,
