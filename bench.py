@@ -12,7 +12,7 @@ Prints ONE JSON line (rank 0) with the driver's contract fields plus
 `roofline` (dominant kernel, HIP-event durations measured in this process)
 and `cpu_baseline` (the CPU oracle on a bounded sample, rank 0 at N=1).
 `full_path` additionally times the full per-frame path (vo_step_batch_dev) over
-a synthetic moving-camera sequence (--full-frames, default 256; 0 skips), and
+a synthetic moving-camera sequence (--full-frames, default 1024; 0 skips), and
 `large` the 1920x1080 / ~8k keypoint configuration (configs[4]) per GPU with the
 i8-MFMA rate of its dense stereo match block (--large-batch, default 8; 0 skips).
 """
@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3)
     ap.add_argument("--concurrency", type=int, default=0, help="forked streams per batch (0: library default)")
-    ap.add_argument("--full-frames", type=int, default=256,
+    ap.add_argument("--full-frames", type=int, default=1024,
                     help="frames of the synthetic sequence timed through the full per-frame path (0: skip)")
     ap.add_argument("--large-batch", type=int, default=8,
                     help="1920x1080 (~8k keypoints) stereo pairs per step for the configs[4] figure (0: skip)")

@@ -1038,7 +1038,7 @@ __global__ __launch_bounds__(256) void k_seg_emit(const Pyramid* __restrict__ py
 // pre[i] <= t < pre[i+1], pre[i+1] = pre[i] + min(counts[i], cap).  The prefix
 // is built once per block in LDS (all threads call flat_setup); flat_find is
 // then a binary search instead of a per-item walk over the images.
-#define VO_FLAT_MAX_IMG 130     // 2 * max_batch(64) + 2 image slots
+#define VO_FLAT_MAX_IMG 258     // 2 * max_batch(128) + 2 image slots
 __device__ __forceinline__ long flat_setup(const int* __restrict__ counts, int cap, int n_img, int* pre)
 {
     const int tid = threadIdx.x, nt = blockDim.x;

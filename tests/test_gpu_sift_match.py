@@ -105,3 +105,41 @@ def test_misaligned_image_pointers(vo, oracle, syn, offset):
             rk, rd = oracle.sift(src)
             _same_kps(k, rk)
             assert np.array_equal(d, rd)
+
+
+def test_batch_128_equals_two_batches_of_64(vo, oracle, syn):
+    """The largest batch (128 frames = 256 images + 2 carry slots in one scale-space arena)
+    gives the same keypoints, descriptors and stereo matches as the same frames in two
+    64-frame calls; frames at both ends are also checked against the oracle."""
+    import torch
+    B = 128
+    L, R = syn.independent_pairs(B)
+    dl = torch.from_numpy(L).cuda()
+    dr = torch.from_numpy(R).cuda()
+    torch.cuda.synchronize()
+
+    def collect(ctx, n):
+        out = []
+        for f in range(n):
+            kl, dsl = ctx.fetch_keypoints(2 * f)
+            kr, dsr = ctx.fetch_keypoints(2 * f + 1)
+            out.append((kl, dsl, kr, dsr, ctx.fetch_stereo_pairs(f)))
+        return out
+
+    big = vo.Context(375, 1242, B)
+    big.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), B)
+    got = collect(big, B)
+    big.close()
+    half = vo.Context(375, 1242, 64)
+    ref = []
+    fs = L[0].size
+    for b0 in (0, 64):
+        half.sift_match_batch_dev(dl.data_ptr() + b0 * fs, dr.data_ptr() + b0 * fs, 64)
+        ref += collect(half, 64)
+    half.close()
+    for f in range(B):
+        for a, b in zip(got[f], ref[f]):
+            assert np.array_equal(a, b), f
+    for f in (0, B - 1):
+        rkl, rdl = oracle.sift(L[f])
+        assert np.array_equal(got[f][0], rkl) and np.array_equal(got[f][1], rdl), f
