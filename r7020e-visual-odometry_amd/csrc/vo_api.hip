@@ -234,8 +234,11 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
         static const int ss_prio = getenv("VO_SS_PRIO") ? atoi(getenv("VO_SS_PRIO")) : 0;
         int lo_p = 0, hi_p = 0;
         hipDeviceGetStreamPriorityRange(&lo_p, &hi_p);
-        const int prio = (k == 0 && ss_prio > 0) ? hi_p : (k == 1 && ss_prio < 0) ? hi_p : lo_p;
-        if ((e = hipStreamCreateWithPriority(&c->sub[k], hipStreamNonBlocking, prio)) != hipSuccess) return bail("stream", e);
+        // default (0): every stream at the default priority -- the forked streams must not
+        // rank below the geometry / copy streams of the pipelined loop body
+        if (ss_prio == 0) e = hipStreamCreateWithFlags(&c->sub[k], hipStreamNonBlocking);
+        else e = hipStreamCreateWithPriority(&c->sub[k], hipStreamNonBlocking, (k == 0) == (ss_prio > 0) ? hi_p : lo_p);
+        if (e != hipSuccess) return bail("stream", e);
         if ((e = hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
     }
     if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("event", e);
