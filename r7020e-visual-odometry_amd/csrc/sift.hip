@@ -1358,18 +1358,23 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
 // ---------------------------------------------------------------------------
 #define DW VO_SIFT_DESCR_W
 #define DN VO_SIFT_DESCR_BINS
-#define DHIST ((DW + 2) * (DW + 2) * (DN + 2))
+// bin stride DN + 1: o0 in [0, DN) so o0 + 1 <= DN -- one wrap bin per cell, folded into bin 0
+#define DBS (DN + 1)
+#define DHIST ((DW + 2) * (DW + 2) * DBS)
 // Histogram copies: lane l adds into copy (l & (DCOPIES-1)), so neighbouring samples
 // (same cell, often the same orientation bin) no longer serialise on one LDS address.
 // Copy stride 360 dwords = 8 mod 32 banks.  u32 fixed point (vo_desc_fx_quant) sums
 // are order-free, so the copies are folded after the loop without changing a bit.
 template <int DCOPIES>
-__global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
+__global__ __launch_bounds__(64, 5) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                              const KpInt* __restrict__ kpi, const int* __restrict__ n_kp,
                                              uint8_t* __restrict__ desc, DescMeta* __restrict__ meta, int kp_cap, int n_img)
 {
     __shared__ uint32_t hfx[DCOPIES * DHIST];
-    __shared__ int rlo[2 * VO_SIFT_DESCR_RMAX + 2], rlen[2 * VO_SIFT_DESCR_RMAX + 2], rstart[2 * VO_SIFT_DESCR_RMAX + 3];
+    // per-row first column (16 bit: |j| <= RMAX) and exclusive sample prefix; a row's length is
+    // rstart[r+1] - rstart[r].  < 8 KB of LDS in all -> 5 one-wave workgroups per SIMD
+    __shared__ int16_t rlo[2 * VO_SIFT_DESCR_RMAX + 2];
+    __shared__ int rstart[2 * VO_SIFT_DESCR_RMAX + 3];
     const int lane = threadIdx.x;
     __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
     const long total = flat_setup(n_kp, kp_cap, n_img, fpre);
@@ -1434,19 +1439,29 @@ __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, con
                 while (jlo <= jhi && !inside(jlo)) ++jlo;
                 while (jhi >= jlo && !inside(jhi)) --jhi;
             }
-            rlo[rr] = jlo;
-            rlen[rr] = jhi >= jlo ? jhi - jlo + 1 : 0;
+            rlo[rr] = (int16_t)jlo;
+            rstart[rr + 1] = jhi >= jlo ? jhi - jlo + 1 : 0;       // row length, prefixed below
         }
         __syncthreads();
-        {   // wave-parallel exclusive prefix over the rows (<= 2*RMAX+1): lane owns a chunk of rows
+        {   // wave-parallel exclusive prefix over the rows (<= 2*RMAX+1): lane owns a chunk of rows.
+            // All lengths are read (rstart[r+1]) before any start is written (rstart[r]): one
+            // wave, LDS operations in program order.
+            constexpr int PER_MAX = (2 * VO_SIFT_DESCR_RMAX + 1 + 63) / 64;
             const int per = (nrows + 63) >> 6, r0w = lane * per;
+            int len[PER_MAX];
             int sum = 0;
-            for (int q = 0; q < per; ++q) if (r0w + q < nrows) sum += rlen[r0w + q];
+#pragma unroll
+            for (int q = 0; q < PER_MAX; ++q) {
+                len[q] = (q < per && r0w + q < nrows) ? rstart[r0w + q + 1] : 0;
+                sum += len[q];
+            }
             int inc = sum;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(inc, o); if (lane >= o) inc += y; }
+            __syncthreads();
             int acc = inc - sum;
-            for (int q = 0; q < per; ++q) if (r0w + q < nrows) { rstart[r0w + q] = acc; acc += rlen[r0w + q]; }
+#pragma unroll
+            for (int q = 0; q < PER_MAX; ++q) if (q < per && r0w + q < nrows) { rstart[r0w + q] = acc; acc += len[q]; }
             if (lane == 63) rstart[nrows] = inc;
         }
         __syncthreads();
@@ -1502,15 +1517,15 @@ __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, con
                 float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
                 float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
                 float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-                uint32_t* h = hc + ((r0 + 1) * (DW + 2) + c0 + 1) * (DN + 2) + o0;
+                uint32_t* h = hc + ((r0 + 1) * (DW + 2) + c0 + 1) * DBS + o0;
                 atomicAdd(h, vo_desc_fx_quant(v_rco000));
                 atomicAdd(h + 1, vo_desc_fx_quant(v_rco001));
-                atomicAdd(h + (DN + 2), vo_desc_fx_quant(v_rco010));
-                atomicAdd(h + (DN + 3), vo_desc_fx_quant(v_rco011));
-                atomicAdd(h + (DW + 2) * (DN + 2), vo_desc_fx_quant(v_rco100));
-                atomicAdd(h + (DW + 2) * (DN + 2) + 1, vo_desc_fx_quant(v_rco101));
-                atomicAdd(h + (DW + 3) * (DN + 2), vo_desc_fx_quant(v_rco110));
-                atomicAdd(h + (DW + 3) * (DN + 2) + 1, vo_desc_fx_quant(v_rco111));
+                atomicAdd(h + DBS, vo_desc_fx_quant(v_rco010));
+                atomicAdd(h + DBS + 1, vo_desc_fx_quant(v_rco011));
+                atomicAdd(h + (DW + 2) * DBS, vo_desc_fx_quant(v_rco100));
+                atomicAdd(h + (DW + 2) * DBS + 1, vo_desc_fx_quant(v_rco101));
+                atomicAdd(h + (DW + 3) * DBS, vo_desc_fx_quant(v_rco110));
+                atomicAdd(h + (DW + 3) * DBS + 1, vo_desc_fx_quant(v_rco111));
                 }
             }
         }
@@ -1522,12 +1537,12 @@ __global__ __launch_bounds__(64) void k_desc(const Pyramid* __restrict__ py, con
             const int kk = lane + 64 * h;
             const int cell = kk / DN, ob = kk - cell * DN;
             const int ci = cell / DW, cj = cell - ci * DW;
-            const int base = ((ci + 1) * (DW + 2) + (cj + 1)) * (DN + 2);
+            const int base = ((ci + 1) * (DW + 2) + (cj + 1)) * DBS;
             uint32_t v = 0;
 #pragma unroll
             for (int cp = 0; cp < DCOPIES; ++cp) {
                 v += hfx[cp * DHIST + base + ob];
-                if (ob < 2) v += hfx[cp * DHIST + base + DN + ob];
+                if (ob == 0) v += hfx[cp * DHIST + base + DN];
             }
             dv[h] = vo_desc_fx_to_float(v);
         }
