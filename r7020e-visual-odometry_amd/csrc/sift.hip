@@ -1363,7 +1363,7 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
 #define DHIST ((DW + 2) * (DW + 2) * DBS)
 // Histogram copies: lane l adds into copy (l & (DCOPIES-1)), so neighbouring samples
 // (same cell, often the same orientation bin) no longer serialise on one LDS address.
-// Copy stride 360 dwords = 8 mod 32 banks.  u32 fixed point (vo_desc_fx_quant) sums
+// Copy stride 324 dwords = 4 mod 32 banks.  u32 fixed point (vo_desc_fx_quant) sums
 // are order-free, so the copies are folded after the loop without changing a bit.
 template <int DCOPIES>
 __global__ __launch_bounds__(64, 5) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
