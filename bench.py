@@ -5,14 +5,20 @@ Workload (BASELINE.json configs[1]): SIFT detect+describe of both images +
 stereo matchFeatures, on 1242x375 synthetic stereo pairs (~2k keypoints per
 image), via libvo.so (hand-written HIP, gfx950).  One step = one batch of
 `--batch` independent stereo frames already resident in HBM.  With --gpus N
-(torchrun, one process per GPU, RCCL) each rank processes its own frames: weak
-scaling, no data-path collective; value = all frames / max-over-ranks time.
+(one process per GPU, RCCL; under torchrun, or bench.py starts torchrun itself
+when WORLD_SIZE is unset) each rank processes its own frames: weak scaling, no
+data-path collective; value = all frames / max-over-ranks time.
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus
 `roofline` (dominant kernel, HIP-event durations measured in this process)
 and `cpu_baseline` (the CPU oracle on a bounded sample, rank 0 at N=1).
-`full_path` additionally times the full per-frame path (vo_step_batch_dev) over
-a synthetic moving-camera sequence (--full-frames, default 1024; 0 skips), and
+`full_path` additionally times the full per-frame path (BASELINE configs[2]/[3]:
+SIFT, stereo match, tracking, DLT, P3P+MSAC with 2048 hypotheses, landmarks) over
+the KITTI-00 trajectory: 4541 frames rendered at 376x1241 along the reference's
+ground truth (street.py), block-sharded over the ranks with a one-frame halo,
+per-frame records and landmark rows all-gathered, poses chained and landmarks
+moved to the world after the chain; it reports the reference's lagged xz error
+(PlotOnMap.m:8-20) and ATE against that trajectory (--seq-frames; 0 skips), and
 `large` the 1920x1080 / ~8k keypoint configuration (configs[4]) per GPU with the
 i8-MFMA rate of its dense stereo match block (--large-batch, default 8; 0 skips).
 """
@@ -50,15 +56,100 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3)
     ap.add_argument("--concurrency", type=int, default=0, help="forked streams per batch (0: library default)")
-    ap.add_argument("--full-frames", type=int, default=1024,
-                    help="frames of the synthetic sequence timed through the full per-frame path (0: skip)")
+    ap.add_argument("--seq-frames", type=int, default=4541,
+                    help="KITTI-00 trajectory frames through the full per-frame path, sharded over the ranks (0: skip)")
+    ap.add_argument("--seq-batch", type=int, default=64, help="frames per vo_step_submit_dev call in the sequence leg")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rendezvous only (gloo, no GPU): rank 0 prints the world size it sees (launcher test)")
     ap.add_argument("--large-batch", type=int, default=8,
                     help="1920x1080 (~8k keypoints) stereo pairs per step for the configs[4] figure (0: skip)")
     return ap.parse_args()
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N ranks with torchrun (one process per
+    GPU, rendezvous on 127.0.0.1) as a child process -- before this process touches the GPU --
+    and return its exit code.  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks):
+    """KITTI-00 (BASELINE configs[2] at N=1, configs[3] at N=8): frames rendered along the
+    reference's ground truth (street.py) into HBM -- each rank only its block + halo -- then
+    timed: the sharded VO loop (vo_step_submit_dev / vo_step_collect, 2048 MSAC hypotheses),
+    the all-gathers of per-frame records and camera-frame landmark rows, the pose chain and
+    the landmark world transform.  Accuracy vs the rendered trajectory: PlotOnMap.m:8-20's
+    lagged xz error and ATE RMSE."""
+    from r7020e_visual_odometry_amd import vo, street, kitti, sharding
+    gt = street.kitti00_gt()
+    n = min(args.seq_frames, len(gt))
+    P0, P1 = street.kitti00_calib()
+    s, e = sharding.shard_range(n, world, rank)
+    h = sharding.halo_start(s)
+    t0 = time.perf_counter()
+    wld = street.kitti00_world(device=f"cuda:{local}", poses=gt)
+    dL = torch.empty((n, street.KITTI_ROWS, street.KITTI_COLS), dtype=torch.uint8, device=f"cuda:{local}")
+    dR = torch.empty_like(dL)
+    street.render_frames(wld, gt, range(h, e), P0, P1, out=(dL[h:e], dR[h:e]))
+    del wld
+    torch.cuda.synchronize()
+    render_s = time.perf_counter() - t0
+    rp = vo.default_ransac_params()
+    rp.max_num_trials = 2048                                   # BASELINE configs[2]
+    SB = args.seq_batch
+    ctx = vo.Context(street.KITTI_ROWS, street.KITTI_COLS, SB, device=local, calib=vo.calib_from(P0, P1), ransac=rp)
+    seq = (dL, dR, P0, P1)
+    ctx.reset()                                                # warm-up: the block's first two batches
+    kitti._pipelined(ctx, kitti.device_batches(dL, dR, SB, h, min(e, h + 2 * SB)), torch.device("cuda", local))
+    torch.cuda.synchronize()
+    dev = torch.device("cuda", local) if dist is not None and dist.get_backend() == "nccl" else None
+    barrier()
+    t0 = time.perf_counter()
+    outs, X, keep = kitti.run_shard(seq, rank, world, SB, local, n, ctx=ctx)
+    if dist is not None:
+        steps = sharding.gather_steps(outs, n, device=dev)
+        X, keep = sharding.gather_landmark_rows(X, keep, device=dev)
+    else:
+        steps = sharding.steps_of(outs)
+    poses, lm = kitti.assemble(steps, X, keep)
+    el = time.perf_counter() - t0
+    barrier()
+    el = max_over_ranks(el)
+    ctx.close()
+    del dL, dR
+    err = kitti.lagged_xz_error(poses, gt[:n])
+    ok = steps["status"][1:] == 0
+    return {"metric": "stereo frames/sec, full per-frame path over the KITTI-00 trajectory (BASELINE configs[2]; configs[3] at 8 GPUs)",
+            "value": n / el, "unit": "stereo frames/s", "frames": n, "frames_per_rank": e - s, "batch": SB,
+            "partition": f"block + one-frame halo over {world} rank(s); all-gather of per-frame records and landmark rows",
+            "rows": street.KITTI_ROWS, "cols": street.KITTI_COLS, "ransac_hypotheses": 2048,
+            "frames_with_pose": int(ok.sum()), "mean_inliers": float(steps["n_inliers"][1:].mean()),
+            "mean_keypoints_per_image": float((steps["n_left"] + steps["n_right"]).mean() / 2),
+            "mean_stereo_matches": float(steps["n_stereo"].mean()), "mean_tracked": float(steps["n_tracked"][1:].mean()),
+            "landmark_rows": int(len(lm)),
+            "accuracy": {"lagged_xz_error_m": {"mean": float(err.mean()), "max": float(err.max()), "final": float(err[-1])},
+                         "ate_rmse_m": kitti.ate_rmse(poses, gt[:n]),
+                         "trajectory_length_m": float(np.linalg.norm(np.diff(gt[:n, :3, 3], axis=0), axis=1).sum()),
+                         "reference": "PlotOnMap.m:8-20 (estimate of frame k vs ground truth of frame k-1); "
+                                      "ATE: positions by frame index, both anchored at frame 0"},
+            "render_s": render_s,
+            "data": "synthetic street world rendered along reference kitti/poses/00.txt with kitti/00/calib.txt P0/P1 "
+                    "(KITTI-00 images are not available)",
+            "note": "timed: sharded loop body + gathers + pose chain + landmark world transform; inputs resident in HBM"}
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     import torch
     import vo_amd  # noqa: F401
     from r7020e_visual_odometry_amd import vo, synthetic as syn, roofline
@@ -70,6 +161,15 @@ def main():
     if os.environ.get("VO_BENCH_SAME_GPU"):
         local = 0
     backend = os.environ.get("VO_BENCH_BACKEND", "nccl")
+    if args.dry_run:
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            dist.barrier()
+            dist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world}))
+        return
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -87,9 +187,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}; reporting {world}", file=sys.stderr)
     B = args.batch
-    # synthetic pairs: rank r renders frames [r*B, (r+1)*B) (seed 0x5EED0000 + frame)
-    L, R = syn.independent_pairs(B, ROWS, COLS, first=rank * B)
+    # synthetic pairs: rank r renders frames [r*B, (r+1)*B) (seed 0x5EED0000 + frame); texture
+    # cell of 15 px puts the oracle at ~2000 keypoints per image (2000 +- 200)
+    L, R = syn.independent_pairs(B, ROWS, COLS, first=rank * B, px_per_cell=syn.BENCH_PX_PER_CELL)
     d_l = torch.from_numpy(L).to(f"cuda:{local}")
     d_r = torch.from_numpy(R).to(f"cuda:{local}")
     torch.cuda.synchronize()
@@ -166,59 +269,10 @@ def main():
     roof["kernel_ms_per_step_isolated"] = {n: round(v[0] / args.profile_steps, 4)
                                            for n, v in sorted(kt_iso.items(), key=lambda kv: -kv[1][0])}
 
-    # ---- BASELINE configs[2] on synthetic data: the full per-frame path (SIFT x2, stereo
-    # match, tracking matches, DLT, P3P+MSAC 2048 hypotheses, landmarks) over a moving-camera
-    # sequence, frames chained across batches of B (device-resident inputs) ----
+    # ---- BASELINE configs[2]/[3]: the full per-frame path over the KITTI-00 trajectory ----
     full = None
-    if args.full_frames > 0:
-        nf = max(1, args.full_frames // B) * B
-        # ping-pong walk (0.25 m/frame forward for 32 frames, then back) keeps the
-        # fronto-parallel planes of the synthetic scene in view, so keypoint counts stay near
-        # the ~2k of configs[1]; the 64-frame loop repeats (frame 64k is frame 0 again)
-        SL, SR, _gt = syn.sequence(32, ROWS, COLS, seed=syn.SEED_BASE + 0x100 * rank, step_m=0.25, yaw_deg=0.1)
-        loop = np.arange(nf) % 64
-        loop = np.where(loop < 32, loop, 63 - loop)
-        SL = np.ascontiguousarray(SL[loop])
-        SR = np.ascontiguousarray(SR[loop])
-        d_sl = torch.from_numpy(SL).to(f"cuda:{local}")
-        d_sr = torch.from_numpy(SR).to(f"cuda:{local}")
-        P1, P2 = syn.calib()
-        fctx = vo.Context(ROWS, COLS, B, device=local, calib=vo.calib_from(P1, P2))
-        fs = SL[0].size
-
-        def run_seq():
-            # pipelined loop body (vo_step_submit_dev / vo_step_collect): batch k+1's SIFT
-            # overlaps batch k's tracking / MSAC / landmarks and its host pose chain
-            fctx.reset()
-            outs = []
-            for b0 in range(0, nf, B):
-                fctx.step_submit_dev(d_sl.data_ptr() + b0 * fs, d_sr.data_ptr() + b0 * fs, B)
-                if fctx.steps_pending() == 2:
-                    outs.append(fctx.step_collect())
-            while fctx.steps_pending():
-                outs.append(fctx.step_collect())
-            return np.concatenate(outs)
-
-        run_seq()
-        torch.cuda.synchronize()
-        barrier()
-        t0 = time.perf_counter()
-        reps = 2
-        for _ in range(reps):
-            outs = run_seq()
-        torch.cuda.synchronize()
-        fel = time.perf_counter() - t0
-        barrier()
-        fel = max_over_ranks(fel)
-        ok = outs["status"][1:] == 0
-        full = {"metric": "stereo frames/sec, full per-frame path (BASELINE configs[2] on synthetic sequence)",
-                "value": nf * reps * world / fel, "unit": "stereo frames/s", "frames_per_rank": nf, "batch": B,
-                "ransac_hypotheses": 2048, "frames_with_pose": int(ok.sum()), "mean_inliers": float(outs["n_inliers"][1:].mean()),
-                "mean_keypoints_per_image": float((outs["n_left"] + outs["n_right"]).mean() / 2),
-                "note": "frames chained through vo_step_submit_dev/vo_step_collect (tracking carried across "
-                        "batches, two batches in flight); includes the per-batch pose/landmark download and host pose chain"}
-        fctx.close()
-        del d_sl, d_sr
+    if args.seq_frames > 0:
+        full = sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks)
 
     # ---- BASELINE configs[4]: 1920x1080 synthetic stereo, ~8k keypoints per image, the dense
     # 8k x 8k descriptor block on the i8 matrix cores (k_match_partial) ----

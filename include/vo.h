@@ -84,9 +84,10 @@ typedef struct {
     float max_ratio;              /* 0.6 */
 } vo_match_params;
 
-/* estworldpose defaults + the BASELINE config (2048 hypotheses). */
+/* estworldpose defaults (VO.m:123-127 calls it with no options: MaxNumTrials 1000).
+ * The BASELINE configs[2] bench passes max_num_trials = 2048 explicitly. */
 typedef struct {
-    int32_t  max_num_trials;      /* 2048 */
+    int32_t  max_num_trials;      /* 1000 (MATLAB default); hypothesis slots the context allocates */
     double   confidence;          /* percent, 99 */
     double   max_reprojection_error; /* pixels, 1 */
     uint32_t seed;                /* Philox key (frame index is mixed in by vo_step) */
@@ -219,6 +220,20 @@ int vo_fetch_tracks(vo_ctx* ctx, int frame, float* old_l, float* cur_l, double* 
 
 /* Landmarks accumulated so far ([rows][3] double, world frame). */
 int vo_get_landmarks(vo_ctx* ctx, double* out, int capacity, int* rows);
+
+/* Sharded sequences: CreateLandmarksFromFeatures.m:17 transforms the
+ * new points by the world pose, which a rank that starts mid-sequence does not know until
+ * the relative poses of every earlier rank are gathered and chained.  With
+ * vo_set_landmark_frame(ctx, 1) the context keeps each appended row in the CAMERA frame
+ * instead: X [rows][3] float (the triangulated point, as CreateLandmarksFromFeatures.m:7
+ * returns it) and keep[rows] (0 = one of the reference's zero rows, :2).  After the chain,
+ * vo_landmarks_to_world applies :17 with the frame's world pose; the result equals the
+ * world-frame rows a single-process run appends, bit for bit.  Mode 0 (default) = world rows
+ * (vo_get_landmarks).  Changing the mode clears the accumulated rows. */
+int vo_set_landmark_frame(vo_ctx* ctx, int camera);
+int vo_get_landmark_rows(vo_ctx* ctx, float* X, uint8_t* keep, int capacity, int* rows);
+/* Host-only, stateless: out[i] = keep[i] ? single(pose * [X[i]; 1]) : 0 (row-major 4x4 pose). */
+int vo_landmarks_to_world(const double pose[16], const float* X, const uint8_t* keep, int n, double* out);
 /* Reset loop state (features, pose, landmarks). */
 int vo_reset(vo_ctx* ctx);
 /* Global index of the next frame (the MSAC Philox key of frame i is

@@ -71,13 +71,22 @@ int oracle_landmarks(const float* l_pos, const float* r_pos, int S, const float*
                      const float* old_r, int K, const double P1[12], const double P2[12],
                      const double pose[16], double* out, int capacity);
 
+/* The same split in two (sharded sequences): camera-frame rows X[rows][3] + keep[rows]
+ * (CreateLandmarksFromFeatures.m:1-16), then the world transform (:17). */
+int oracle_landmark_rows(const float* l_pos, const float* r_pos, int S, const float* old_l,
+                         const float* old_r, int K, const double P1[12], const double P2[12],
+                         float* X, uint8_t* keep, int capacity);
+void oracle_landmarks_to_world(const double pose[16], const float* X, const uint8_t* keep, int n, double* out);
+
 /* Whole loop over a sequence (VO.m:64-232): frames [F][rows*cols] u8 tightly
  * packed.  outs[F]; landmarks appended to lm_out (capacity rows). Frame f uses
- * MSAC key key0 + f (key0 = global index of frame 0).  Returns landmark rows. */
+ * MSAC key key0 + f (key0 = global index of frame 0).  Returns landmark rows.
+ * With lm_cam_X/lm_cam_keep non-NULL the rows are appended there in the camera frame
+ * instead (lm_out unused). */
 long oracle_run_sequence(const uint8_t* lefts, const uint8_t* rights, int F, int rows, int cols,
                          const vo_calib* calib, const vo_sift_params* sp, const vo_match_params* mp,
                          const vo_ransac_params* rp, vo_step_out* outs, double* lm_out, long lm_cap,
-                         uint32_t key0);
+                         uint32_t key0, float* lm_cam_X, uint8_t* lm_cam_keep);
 
 /* spec primitive evaluation for KATs (spec_eval.c) */
 void oracle_spec_eval(int fn, const double* in, double* out, int n);

@@ -17,6 +17,9 @@ import numpy as np
 
 HERE = Path(__file__).resolve().parent
 LIB = HERE / "build" / "liboracle.so"
+# the same sources built with -DVO_CV_LITERAL: OpenCV-literal float SIFT + MATLAB-literal
+# float matcher (the reference implementations the spec's deterministic choices depart from)
+LIB_CV = HERE / "build" / "liboracle_cv.so"
 
 
 class SiftParams(C.Structure):
@@ -61,7 +64,9 @@ def match_params() -> MatchParams:
     return MatchParams(1.0, 0.6)
 
 
-def ransac_params(trials: int = 2048, seed: int = 0x5EED) -> RansacParams:
+def ransac_params(trials: int = 1000, seed: int = 0x5EED) -> RansacParams:
+    """estworldpose defaults as VO.m:123-127 calls it (MaxNumTrials 1000); the BASELINE
+    configs[2] bench uses trials=2048."""
     return RansacParams(trials, 99.0, 1.0, seed)
 
 
@@ -74,7 +79,7 @@ def calib_from(P1: np.ndarray, P2: np.ndarray) -> Calib:
     return c
 
 
-_lib = None
+_libs: dict = {}
 
 
 def build() -> Path:
@@ -82,12 +87,12 @@ def build() -> Path:
     return LIB
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not LIB.exists():
+def lib(cv: bool = False):
+    path = LIB_CV if cv else LIB
+    if path not in _libs:
+        if not path.exists():
             build()
-        L = C.CDLL(str(LIB))
+        L = C.CDLL(str(path))
         P = C.POINTER
         L.oracle_sift.argtypes = [P(C.c_uint8), C.c_int, C.c_int, C.c_int, P(SiftParams), P(Keypoint), P(C.c_uint8), C.c_int]
         L.oracle_sift.restype = C.c_int
@@ -110,7 +115,9 @@ def lib():
                                        P(C.c_double), P(C.c_double), P(C.c_double), P(C.c_double), C.c_int]
         L.oracle_run_sequence.argtypes = [P(C.c_uint8), P(C.c_uint8), C.c_int, C.c_int, C.c_int, P(Calib), P(SiftParams),
                                           P(MatchParams), P(RansacParams), P(StepOut), P(C.c_double), C.c_long,
-                                          C.c_uint32]
+                                          C.c_uint32, P(C.c_float), P(C.c_uint8)]
+        L.oracle_landmarks_to_world.argtypes = [P(C.c_double), P(C.c_float), P(C.c_uint8), C.c_int, P(C.c_double)]
+        L.oracle_landmarks_to_world.restype = None
         L.oracle_spec_eval.argtypes = [C.c_int, P(C.c_double), P(C.c_double), C.c_int]
         L.oracle_spec_eval.restype = None
         L.oracle_philox.argtypes = [C.c_uint32] * 6 + [P(C.c_uint32)]
@@ -119,22 +126,22 @@ def lib():
         L.oracle_run_sequence.restype = C.c_long
         L.oracle_sift_match_pair.argtypes = [P(C.c_uint8), P(C.c_uint8), C.c_int, C.c_int, P(SiftParams), P(MatchParams),
                                              P(C.c_int), P(C.c_int)]
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 def _p(a, t):
     return a.ctypes.data_as(C.POINTER(t))
 
 
-def sift(img: np.ndarray, params: SiftParams | None = None):
+def sift(img: np.ndarray, params: SiftParams | None = None, cv: bool = False):
     """-> (keypoints structured array, descriptors [n,128] u8)"""
     img = np.ascontiguousarray(img, np.uint8)
     p = params or sift_params()
     cap = p.max_keypoints
     kps = np.zeros(cap, KP_DTYPE)
     desc = np.zeros((cap, 128), np.uint8)
-    n = lib().oracle_sift(_p(img, C.c_uint8), img.shape[0], img.shape[1], img.shape[1], C.byref(p),
+    n = lib(cv).oracle_sift(_p(img, C.c_uint8), img.shape[0], img.shape[1], img.shape[1], C.byref(p),
                           kps.ctypes.data_as(C.POINTER(Keypoint)), _p(desc, C.c_uint8), cap)
     n = min(n, cap)
     return kps[:n].copy(), desc[:n].copy()
@@ -170,12 +177,12 @@ def pyramid(img: np.ndarray, params: SiftParams | None = None) -> np.ndarray:
     return out
 
 
-def match(F1: np.ndarray, F2: np.ndarray, params: MatchParams | None = None) -> np.ndarray:
+def match(F1: np.ndarray, F2: np.ndarray, params: MatchParams | None = None, cv: bool = False) -> np.ndarray:
     F1 = np.ascontiguousarray(F1, np.uint8)
     F2 = np.ascontiguousarray(F2, np.uint8)
     cap = max(F1.shape[0], 1)
     pairs = np.zeros((cap, 2), np.uint32)
-    n = lib().oracle_match(_p(F1, C.c_uint8), F1.shape[0], _p(F2, C.c_uint8), F2.shape[0],
+    n = lib(cv).oracle_match(_p(F1, C.c_uint8), F1.shape[0], _p(F2, C.c_uint8), F2.shape[0],
                            C.byref(params or match_params()), _p(pairs, C.c_uint32), cap)
     return pairs[:n].copy()
 
@@ -243,18 +250,38 @@ STEP_DTYPE = np.dtype([("status", "<i4"), ("n_left", "<i4"), ("n_right", "<i4"),
                        ("rel_pose", "<f8", (4, 4)), ("pose", "<f8", (4, 4))])
 
 
-def run_sequence(L, R, P1, P2, sp=None, mp=None, rp=None, lm_cap: int = 1 << 20, key0: int = 0):
+def run_sequence(L, R, P1, P2, sp=None, mp=None, rp=None, lm_cap: int = 1 << 20, key0: int = 0,
+                 camera_rows: bool = False, cv: bool = False):
+    """VO.m loop -> (outs, landmarks [L, 3] world); with camera_rows=True the landmark rows
+    stay in the camera frame: (outs, (X [L, 3] float32, keep [L] bool))."""
     L = np.ascontiguousarray(L, np.uint8)
     R = np.ascontiguousarray(R, np.uint8)
     F, rows, cols = L.shape
     outs = np.zeros(F, STEP_DTYPE)
     lm = np.zeros((lm_cap, 3))
     cal = calib_from(P1, P2)
-    n = lib().oracle_run_sequence(_p(L, C.c_uint8), _p(R, C.c_uint8), F, rows, cols, C.byref(cal),
+    X = np.zeros((lm_cap, 3), np.float32) if camera_rows else None
+    keep = np.zeros(lm_cap, np.uint8) if camera_rows else None
+    n = lib(cv).oracle_run_sequence(_p(L, C.c_uint8), _p(R, C.c_uint8), F, rows, cols, C.byref(cal),
                                   C.byref(sp or sift_params()), C.byref(mp or match_params()),
                                   C.byref(rp or ransac_params()), outs.ctypes.data_as(C.POINTER(StepOut)),
-                                  _p(lm, C.c_double), lm_cap, key0)
+                                  _p(lm, C.c_double), lm_cap, key0,
+                                  _p(X, C.c_float) if camera_rows else None,
+                                  _p(keep, C.c_uint8) if camera_rows else None)
+    if camera_rows:
+        return outs, (X[:n].copy(), keep[:n].astype(bool))
     return outs, lm[:n].copy()
+
+
+def landmarks_to_world(pose, X, keep) -> np.ndarray:
+    """CreateLandmarksFromFeatures.m:17 on camera-frame rows (keep=False: zero row)."""
+    pose = np.ascontiguousarray(pose, np.float64).reshape(4, 4)
+    X = np.ascontiguousarray(X, np.float32).reshape(-1, 3)
+    k = np.ascontiguousarray(keep, np.uint8).reshape(-1)
+    out = np.zeros((X.shape[0], 3))
+    lib().oracle_landmarks_to_world(_p(pose, C.c_double), _p(X, C.c_float), _p(k, C.c_uint8), X.shape[0],
+                                    _p(out, C.c_double))
+    return out
 
 
 def sift_match_pair(left, right, sp=None, mp=None):

@@ -12,16 +12,54 @@
  *   - separable Gaussian, reflect-101, symmetric fmaf accumulation order,
  *   - Cramer's rule in double for the 3x3 Newton step,
  *   - vo_spec.h exp/atan2/sincos,
- *   - orientation/descriptor histograms summed in 2^-20 fixed point,
+ *   - orientation/descriptor histograms summed in 2^-10 fixed point (vo_spec.h
+ *     VO_DESC_FX_SCALE = 1024: every contribution pre-scaled by 2^10, rounded
+ *     to an integer, summed exactly),
  *   - descriptor norms as a 128 -> 1 pairwise tree,
  *   - keypoint order = (octave, layer, row, col) scan order, then peak bin.
  * Everything is plain C99 compiled with -ffp-contract=off.
+ *
+ * Built a second time with -DVO_CV_LITERAL (build/liboracle_cv.so) it is instead
+ * the OpenCV-literal float SIFT those choices depart from: histograms accumulated
+ * in float in OpenCV's sample order, OpenCV's fastAtan2 polynomial, libm
+ * expf/sinf/cosf/powf, sequential float norms, no descriptor-radius cap, and
+ * KeyPointsFilter::removeDuplicatedSorted (sort by x, y, size, angle; drop
+ * exact duplicates).  tests/test_spec_divergence.py measures how far the spec
+ * is from it.
  */
 #include <stdlib.h>
 #include <string.h>
 #include <math.h>
 #include "oracle.h"
 #include "vo_spec.h"
+
+#ifdef VO_CV_LITERAL
+#include <float.h>
+/* OpenCV's cv::fastAtan2 (degrees in [0, 360)): the published 7th-order polynomial */
+static float cv_fast_atan2(float y, float x)
+{
+    const float p1 = 0.9997878412794807f * 57.29577951308232f, p3 = -0.3258083974640975f * 57.29577951308232f;
+    const float p5 = 0.1555786518463281f * 57.29577951308232f, p7 = -0.04432655554792128f * 57.29577951308232f;
+    float ax = fabsf(x), ay = fabsf(y), a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.0f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.0f - a;
+    if (y < 0) a = 360.0f - a;
+    return a;
+}
+#define SIFT_EXPF(x) expf(x)
+#define SIFT_ATAN2(y, x) cv_fast_atan2((y), (x))
+#else
+#define SIFT_EXPF(x) vo_expf(x)
+#define SIFT_ATAN2(y, x) vo_atan2_deg((y), (x))
+#endif
 
 int oracle_num_octaves(int rows, int cols, int upsample) { return vo_num_octaves(rows, cols, upsample); }
 
@@ -230,7 +268,11 @@ static int refine(const pyramid_t* py, int o, int layer, int r, int c, const vo_
         out->xo = (float)c + xc;
         out->yo = (float)r + xr;
         out->xi = xi;
+#ifdef VO_CV_LITERAL
+        out->scl = p->sigma * powf(2.0f, ((float)layer + xi) / (float)L);
+#else
         out->scl = p->sigma * vo_expf(((float)layer + xi) / (float)L * 0.693147181f);
+#endif
         out->response = fabsf(contr);
         out->r = r; out->c = c; out->layer = layer;
     }
@@ -245,8 +287,13 @@ static int orientations(const float* img, int rows, int cols, int r, int c, floa
     int radius = vo_round(VO_SIFT_ORI_RADIUS * scl);
     float sigw = VO_SIFT_ORI_SIG * scl;
     float expf_scale = -1.0f / (2.0f * sigw * sigw);
+#ifdef VO_CV_LITERAL
+    float hfl[VO_SIFT_ORI_BINS];
+    memset(hfl, 0, sizeof(hfl));
+#else
     uint64_t hfx[VO_SIFT_ORI_BINS];
     memset(hfx, 0, sizeof(hfx));
+#endif
     for (int i = -radius; i <= radius; ++i) {
         int y = r + i;
         if (y <= 0 || y >= rows - 1) continue;
@@ -255,17 +302,25 @@ static int orientations(const float* img, int rows, int cols, int r, int c, floa
             if (x <= 0 || x >= cols - 1) continue;
             float dx = AT(img, cols, y, x + 1) - AT(img, cols, y, x - 1);
             float dy = AT(img, cols, y - 1, x) - AT(img, cols, y + 1, x);
-            float w = vo_expf((float)(i * i + j * j) * expf_scale);
+            float w = SIFT_EXPF((float)(i * i + j * j) * expf_scale);
             float mag = sqrtf(dx * dx + dy * dy);
-            float ori = vo_atan2_deg(dy, dx);
+            float ori = SIFT_ATAN2(dy, dx);
             int bin = vo_round((float)n / 360.0f * ori);
             if (bin >= n) bin -= n;
             if (bin < 0) bin += n;
+#ifdef VO_CV_LITERAL
+            hfl[bin] += w * mag;
+#else
             hfx[bin] += vo_desc_fx_quant((w * mag) * VO_DESC_FX_SCALE);
+#endif
         }
     }
     float t[VO_SIFT_ORI_BINS], hist[VO_SIFT_ORI_BINS];
+#ifdef VO_CV_LITERAL
+    for (int k = 0; k < n; ++k) t[k] = hfl[k];
+#else
     for (int k = 0; k < n; ++k) t[k] = vo_hist_fx_to_float(hfx[k]);
+#endif
     float maxval = 0.0f;
     for (int k = 0; k < n; ++k) {
         float m2 = t[(k + n - 2) % n], m1 = t[(k + n - 1) % n], p1 = t[(k + 1) % n], p2 = t[(k + 2) % n];
@@ -296,17 +351,29 @@ static void descriptor(const float* img, int rows, int cols, float xo, float yo,
     if (fabsf(ori - 360.0f) < VO_FLT_EPSILON) ori = 0.0f;
     int px = vo_round(xo), py = vo_round(yo);
     float sin_t, cos_t;
+#ifdef VO_CV_LITERAL
+    cos_t = cosf(ori * (float)(3.14159265358979323846 / 180));
+    sin_t = sinf(ori * (float)(3.14159265358979323846 / 180));
+#else
     vo_sincos_deg(ori, &sin_t, &cos_t);
+#endif
     const float bins_per_deg = (float)n / 360.0f;
     const float exp_scale = -1.0f / ((float)(d * d) * 0.5f);
     float hist_width = VO_SIFT_DESCR_SCL * scl;
     int radius = vo_round(hist_width * 1.4142135623730951f * (float)(d + 1) * 0.5f);
     int rmax = (int)sqrt((double)cols * cols + (double)rows * rows);
     if (radius > rmax) radius = rmax;
+#ifdef VO_CV_LITERAL
+    typedef float hist_t;                 /* OpenCV: float bins, no radius cap */
+#define HQ(v) (v)
+#else
     if (radius > VO_SIFT_DESCR_RMAX) radius = VO_SIFT_DESCR_RMAX;
+    typedef uint32_t hist_t;
+#define HQ(v) vo_desc_fx_quant(v)
+#endif
     cos_t = cos_t / hist_width;
     sin_t = sin_t / hist_width;
-    uint32_t hfx[(VO_SIFT_DESCR_W + 2) * (VO_SIFT_DESCR_W + 2) * (VO_SIFT_DESCR_BINS + 2)];
+    hist_t hfx[(VO_SIFT_DESCR_W + 2) * (VO_SIFT_DESCR_W + 2) * (VO_SIFT_DESCR_BINS + 2)];
     memset(hfx, 0, sizeof(hfx));
     for (int i = -radius; i <= radius; ++i) {
         for (int j = -radius; j <= radius; ++j) {
@@ -319,9 +386,13 @@ static void descriptor(const float* img, int rows, int cols, float xo, float yo,
                   r > 0 && r < rows - 1 && c > 0 && c < cols - 1)) continue;
             float dx = AT(img, cols, r, c + 1) - AT(img, cols, r, c - 1);
             float dy = AT(img, cols, r - 1, c) - AT(img, cols, r + 1, c);
-            float w = vo_expf((c_rot * c_rot + r_rot * r_rot) * exp_scale);
-            float ang = vo_atan2_deg(dy, dx);
+            float w = SIFT_EXPF((c_rot * c_rot + r_rot * r_rot) * exp_scale);
+            float ang = SIFT_ATAN2(dy, dx);
+#ifdef VO_CV_LITERAL
+            float mag = sqrtf(dx * dx + dy * dy) * w;
+#else
             float mag = (sqrtf(dx * dx + dy * dy) * w) * VO_DESC_FX_SCALE;   /* exact power-of-two pre-scale */
+#endif
             float obin = (ang - ori) * bins_per_deg;
             int r0 = vo_floor(rbin), c0 = vo_floor(cbin), o0 = vo_floor(obin);
             rbin -= (float)r0; cbin -= (float)c0; obin -= (float)o0;
@@ -335,14 +406,14 @@ static void descriptor(const float* img, int rows, int cols, float xo, float yo,
             float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
             float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
             int idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
-            hfx[idx] += vo_desc_fx_quant(v_rco000);
-            hfx[idx + 1] += vo_desc_fx_quant(v_rco001);
-            hfx[idx + (n + 2)] += vo_desc_fx_quant(v_rco010);
-            hfx[idx + (n + 3)] += vo_desc_fx_quant(v_rco011);
-            hfx[idx + (d + 2) * (n + 2)] += vo_desc_fx_quant(v_rco100);
-            hfx[idx + (d + 2) * (n + 2) + 1] += vo_desc_fx_quant(v_rco101);
-            hfx[idx + (d + 3) * (n + 2)] += vo_desc_fx_quant(v_rco110);
-            hfx[idx + (d + 3) * (n + 2) + 1] += vo_desc_fx_quant(v_rco111);
+            hfx[idx] += HQ(v_rco000);
+            hfx[idx + 1] += HQ(v_rco001);
+            hfx[idx + (n + 2)] += HQ(v_rco010);
+            hfx[idx + (n + 3)] += HQ(v_rco011);
+            hfx[idx + (d + 2) * (n + 2)] += HQ(v_rco100);
+            hfx[idx + (d + 2) * (n + 2) + 1] += HQ(v_rco101);
+            hfx[idx + (d + 3) * (n + 2)] += HQ(v_rco110);
+            hfx[idx + (d + 3) * (n + 2) + 1] += HQ(v_rco111);
         }
     }
     float dst[VO_DESC_LEN];
@@ -351,8 +422,22 @@ static void descriptor(const float* img, int rows, int cols, float xo, float yo,
             int idx = ((i + 1) * (d + 2) + (j + 1)) * (n + 2);
             hfx[idx] += hfx[idx + n];
             hfx[idx + 1] += hfx[idx + n + 1];
+#ifdef VO_CV_LITERAL
+            for (int k = 0; k < n; ++k) dst[(i * d + j) * n + k] = hfx[idx + k];
+#else
             for (int k = 0; k < n; ++k) dst[(i * d + j) * n + k] = vo_desc_fx_to_float(hfx[idx + k]);
+#endif
         }
+#undef HQ
+#ifdef VO_CV_LITERAL
+    /* OpenCV: sequential float sums */
+    float nrm2 = 0;
+    for (int k = 0; k < VO_DESC_LEN; ++k) nrm2 += dst[k] * dst[k];
+    float thr = sqrtf(nrm2) * VO_SIFT_DESCR_MAG_THR;
+    nrm2 = 0;
+    for (int k = 0; k < VO_DESC_LEN; ++k) { float v = dst[k] < thr ? dst[k] : thr; dst[k] = v; nrm2 += v * v; }
+    float nrm = sqrtf(nrm2);
+#else
     /* norms: pairwise tree 128 -> 1 (stride 64, 32, ..., 1) */
     float s[VO_DESC_LEN];
     for (int k = 0; k < VO_DESC_LEN; ++k) s[k] = dst[k] * dst[k];
@@ -361,12 +446,53 @@ static void descriptor(const float* img, int rows, int cols, float xo, float yo,
     for (int k = 0; k < VO_DESC_LEN; ++k) { float v = dst[k] < thr ? dst[k] : thr; dst[k] = v; s[k] = v * v; }
     for (int st = 64; st >= 1; st >>= 1) for (int k = 0; k < st; ++k) s[k] = s[k] + s[k + st];
     float nrm = sqrtf(s[0]);
+#endif
     float scale = VO_SIFT_DESCR_INT_FCTR / (nrm > VO_FLT_EPSILON ? nrm : VO_FLT_EPSILON);
     for (int k = 0; k < VO_DESC_LEN; ++k) {
         float v = rintf(dst[k] * scale);
         out[k] = (uint8_t)(v < 0.0f ? 0 : v > 255.0f ? 255 : (int)v);
     }
 }
+
+#ifdef VO_CV_LITERAL
+/* KeyPointsFilter::removeDuplicatedSorted: sort by (x, y, size, angle), drop entries whose
+ * x, y, size and angle all equal the previous kept one (descriptors follow their keypoint) */
+static const vo_keypoint* g_sort_kps;
+static int cv_kp_less(const void* a, const void* b)
+{
+    const vo_keypoint *p = &g_sort_kps[*(const int*)a], *q = &g_sort_kps[*(const int*)b];
+    if (p->x != q->x) return p->x < q->x ? -1 : 1;
+    if (p->y != q->y) return p->y < q->y ? -1 : 1;
+    if (p->size != q->size) return p->size > q->size ? -1 : 1;    /* OpenCV: larger size first */
+    if (p->angle != q->angle) return p->angle < q->angle ? -1 : 1;
+    if (p->response != q->response) return p->response > q->response ? -1 : 1;
+    if (p->octave != q->octave) return p->octave > q->octave ? -1 : 1;
+    return *(const int*)a - *(const int*)b;
+}
+
+static int cv_remove_duplicated_sorted(vo_keypoint* kps, uint8_t* desc, int n)
+{
+    int* ord = (int*)malloc(sizeof(int) * (n + 1));
+    for (int i = 0; i < n; ++i) ord[i] = i;
+    g_sort_kps = kps;
+    qsort(ord, n, sizeof(int), cv_kp_less);
+    vo_keypoint* k2 = (vo_keypoint*)malloc(sizeof(vo_keypoint) * (n + 1));
+    uint8_t* d2 = desc ? (uint8_t*)malloc((size_t)(n + 1) * VO_DESC_LEN) : NULL;
+    int m = 0;
+    for (int i = 0; i < n; ++i) {
+        const vo_keypoint* k = &kps[ord[i]];
+        if (m > 0 && k->x == k2[m - 1].x && k->y == k2[m - 1].y && k->size == k2[m - 1].size && k->angle == k2[m - 1].angle)
+            continue;
+        k2[m] = *k;
+        if (d2) memcpy(d2 + (size_t)m * VO_DESC_LEN, desc + (size_t)ord[i] * VO_DESC_LEN, VO_DESC_LEN);
+        m++;
+    }
+    memcpy(kps, k2, sizeof(vo_keypoint) * m);
+    if (d2) memcpy(desc, d2, (size_t)m * VO_DESC_LEN);
+    free(ord); free(k2); free(d2);
+    return m;
+}
+#endif
 
 /* ---------------- detect + describe ---------------- */
 int oracle_sift(const uint8_t* img, int rows, int cols, int ld, const vo_sift_params* p,
@@ -433,5 +559,8 @@ int oracle_sift(const uint8_t* img, int rows, int cols, int ld, const vo_sift_pa
         }
     }
     free_pyramid(&py);
+#ifdef VO_CV_LITERAL
+    if (count <= capacity) count = cv_remove_duplicated_sorted(kps, desc, count);
+#endif
     return count;
 }

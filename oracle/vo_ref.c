@@ -36,6 +36,49 @@ static float ssd_u8(const uint8_t* a, const uint8_t* b, float ia, float ib)
     return 2.0f - 2.0f * c;
 }
 
+#ifdef VO_CV_LITERAL
+/* MATLAB-literal matchFeatures (Exhaustive, SSD, Prenormalized false): single rows
+ * normalised to unit L2 in float, SSD as a sequential float sum of squared differences */
+static void unit_rows(const uint8_t* A, const int* ia, int n, float* out)
+{
+    for (int i = 0; i < n; ++i) {
+        const uint8_t* a = A + (size_t)ia[i] * VO_DESC_LEN;
+        float s = 0;
+        for (int k = 0; k < VO_DESC_LEN; ++k) s += (float)a[k] * (float)a[k];
+        float nrm = sqrtf(s);
+        for (int k = 0; k < VO_DESC_LEN; ++k) out[(size_t)i * VO_DESC_LEN + k] = nrm > 0 ? (float)a[k] / nrm : 0.0f;
+    }
+}
+
+static int match_idx(const uint8_t* A, const int* ia, int n1, const uint8_t* B, const int* ib, int n2,
+                     const vo_match_params* p, int* out1, int* out2)
+{
+    float* fa = (float*)malloc(sizeof(float) * VO_DESC_LEN * (n1 > 0 ? n1 : 1));
+    float* fb = (float*)malloc(sizeof(float) * VO_DESC_LEN * (n2 > 0 ? n2 : 1));
+    unit_rows(A, ia, n1, fa);
+    unit_rows(B, ib, n2, fb);
+    const float T = p->match_threshold * 0.04f;
+    int P = 0;
+    for (int i = 0; i < n1; ++i) {
+        const float* a = fa + (size_t)i * VO_DESC_LEN;
+        float best = INFINITY, second = INFINITY;
+        int bidx = -1;
+        for (int j = 0; j < n2; ++j) {
+            const float* b = fb + (size_t)j * VO_DESC_LEN;
+            float s = 0;
+            for (int k = 0; k < VO_DESC_LEN; ++k) { float t = a[k] - b[k]; s += t * t; }
+            if (s < best) { second = best; best = s; bidx = j; }
+            else if (s < second) second = s;
+        }
+        if (bidx < 0) continue;
+        if (!(best <= T)) continue;
+        if (!(best / second <= p->max_ratio)) continue;
+        out1[P] = i; out2[P] = bidx; P++;
+    }
+    free(fa); free(fb);
+    return P;
+}
+#else
 /* generic match on gathered rows: F1 rows = A[ia[i]], F2 rows = B[ib[j]] */
 static int match_idx(const uint8_t* A, const int* ia, int n1, const uint8_t* B, const int* ib, int n2,
                      const vo_match_params* p, int* out1, int* out2)
@@ -63,6 +106,7 @@ static int match_idx(const uint8_t* A, const int* ia, int n1, const uint8_t* B, 
     free(inb);
     return P;
 }
+#endif
 
 int oracle_match(const uint8_t* F1, int n1, const uint8_t* F2, int n2, const vo_match_params* p,
                  uint32_t* pairs, int capacity)
@@ -491,9 +535,12 @@ int oracle_estworldpose(const double* img, const double* world, int n, const dou
 /* ======================================================================= */
 /* landmarks: VO.m:145-160 + CreateLandmarksFromFeatures.m                  */
 /* ======================================================================= */
-int oracle_landmarks(const float* l_pos, const float* r_pos, int S, const float* old_l,
-                     const float* old_r, int K, const double P1[12], const double P2[12],
-                     const double pose[16], double* out, int capacity)
+/* CreateLandmarksFromFeatures.m:1-16 in the camera frame: X[rows][3] (the triangulated
+ * point, single-rounded as dlt_point returns it) and keep[rows] (0 = zero row).  Returns
+ * rows; only min(rows, capacity) are written. */
+int oracle_landmark_rows(const float* l_pos, const float* r_pos, int S, const float* old_l,
+                         const float* old_r, int K, const double P1[12], const double P2[12],
+                         float* X_out, uint8_t* keep, int capacity)
 {
     int* idx = (int*)malloc(sizeof(int) * (S + 1));
     int M = 0;
@@ -507,27 +554,46 @@ int oracle_landmarks(const float* l_pos, const float* r_pos, int S, const float*
     }
     /* landmarks = zeros(size(features_l,2),3) -> 2 rows; grows to last kept odd i */
     int rows = 2;
+    for (int r = 0; r < 2 && r < capacity; ++r) { keep[r] = 0; X_out[3 * r] = X_out[3 * r + 1] = X_out[3 * r + 2] = 0.0f; }
     for (int i = 0; i < M; i += 2) {   /* 1-based odd i <-> 0-based even */
         double X[3];
         dlt_point(l_pos[2 * idx[i]], l_pos[2 * idx[i] + 1], r_pos[2 * idx[i]], r_pos[2 * idx[i] + 1], P1, P2, X);
         if (X[2] < 0) continue;
         if (X[2] > 80) continue;
+        for (int r = rows; r < i + 1 && r < capacity; ++r) { keep[r] = 0; X_out[3 * r] = X_out[3 * r + 1] = X_out[3 * r + 2] = 0.0f; }
         if (i + 1 > rows) rows = i + 1;
-    }
-    if (out) {
-        for (int r = 0; r < rows && r < capacity; ++r) out[3 * r] = out[3 * r + 1] = out[3 * r + 2] = 0.0;
-        for (int i = 0; i < M; i += 2) {
-            double X[3];
-            dlt_point(l_pos[2 * idx[i]], l_pos[2 * idx[i] + 1], r_pos[2 * idx[i]], r_pos[2 * idx[i] + 1], P1, P2, X);
-            if (X[2] < 0 || X[2] > 80) continue;
-            if (i >= capacity) continue;
-            for (int a = 0; a < 3; ++a) {
-                double w = pose[4 * a] * X[0] + pose[4 * a + 1] * X[1] + pose[4 * a + 2] * X[2] + pose[4 * a + 3];
-                out[3 * i + a] = (double)(float)w;
-            }
+        if (i < capacity) {
+            keep[i] = 1;
+            for (int a = 0; a < 3; ++a) X_out[3 * i + a] = (float)X[a];
         }
     }
     free(idx);
+    return rows;
+}
+
+/* CreateLandmarksFromFeatures.m:17: world = single(pose * [X; 1]) for kept rows. */
+void oracle_landmarks_to_world(const double pose[16], const float* X, const uint8_t* keep, int n, double* out)
+{
+    for (int m = 0; m < n; ++m)
+        for (int a = 0; a < 3; ++a) {
+            if (!keep[m]) { out[3 * m + a] = 0.0; continue; }
+            const double x0 = X[3 * m], x1 = X[3 * m + 1], x2 = X[3 * m + 2];
+            double w = pose[4 * a] * x0 + pose[4 * a + 1] * x1 + pose[4 * a + 2] * x2 + pose[4 * a + 3];
+            out[3 * m + a] = (double)(float)w;
+        }
+}
+
+int oracle_landmarks(const float* l_pos, const float* r_pos, int S, const float* old_l,
+                     const float* old_r, int K, const double P1[12], const double P2[12],
+                     const double pose[16], double* out, int capacity)
+{
+    int cap = S + 2;
+    float* X = (float*)malloc(sizeof(float) * 3 * cap);
+    uint8_t* keep = (uint8_t*)malloc(cap);
+    int rows = oracle_landmark_rows(l_pos, r_pos, S, old_l, old_r, K, P1, P2, X, keep, cap);
+    if (out) oracle_landmarks_to_world(pose, X, keep, rows < capacity ? rows : capacity, out);
+    free(X);
+    free(keep);
     return rows;
 }
 
@@ -548,7 +614,7 @@ static const double I4[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
 long oracle_run_sequence(const uint8_t* lefts, const uint8_t* rights, int F, int rows, int cols,
                          const vo_calib* calib, const vo_sift_params* sp, const vo_match_params* mp,
                          const vo_ransac_params* rp, vo_step_out* outs, double* lm_out, long lm_cap,
-                         uint32_t key0)
+                         uint32_t key0, float* lm_cam_X, uint8_t* lm_cam_keep)
 {
     int cap = sp->max_keypoints;
     vo_keypoint *kl = malloc(sizeof(vo_keypoint) * cap), *kr = malloc(sizeof(vo_keypoint) * cap);
@@ -602,8 +668,14 @@ long oracle_run_sequence(const uint8_t* lefts, const uint8_t* rights, int F, int
                 mat4_mul(pose, T, pose);
             }
             long room = lm_cap - lm_rows;
-            int rows_added = oracle_landmarks(sl, sr, S, ol, orr, Kt, calib->P1, calib->P2, pose,
-                                              lm_out ? lm_out + 3 * lm_rows : NULL, room > 0 ? (int)(room < 0x7fffffff ? room : 0x7fffffff) : 0);
+            int room_i = room > 0 ? (int)(room < 0x7fffffff ? room : 0x7fffffff) : 0;
+            int rows_added;
+            if (lm_cam_X)        /* camera-frame rows for a sharded run (world transform after the chain) */
+                rows_added = oracle_landmark_rows(sl, sr, S, ol, orr, Kt, calib->P1, calib->P2,
+                                                  lm_cam_X + 3 * lm_rows, lm_cam_keep + lm_rows, room_i);
+            else
+                rows_added = oracle_landmarks(sl, sr, S, ol, orr, Kt, calib->P1, calib->P2, pose,
+                                              lm_out ? lm_out + 3 * lm_rows : NULL, room_i);
             o->n_landmarks = rows_added;
             lm_rows += rows_added;
         }

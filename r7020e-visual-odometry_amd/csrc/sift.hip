@@ -304,103 +304,6 @@ __global__ __launch_bounds__(256) void k_blur_fused(const float* __restrict__ sr
 }
 
 // ---------------------------------------------------------------------------
-// Persistent, software-pipelined level blur (MODE 0, compiled radius).  Same
-// per-output arithmetic as k_blur_fused; each block walks tiles
-// T, T+grid, ...: the global loads of tile T+grid are issued into registers
-// right after tile T is in LDS, so they are in flight during T's row and
-// column passes (async-STAGE split), instead of every tile exposing a full
-// HBM round trip behind a barrier.
-// ---------------------------------------------------------------------------
-template <int RAD>
-__global__ __launch_bounds__(256) void k_blur_pipe(const float* __restrict__ src, size_t plane, size_t dplane, int pitch, int R, int C,
-                                                   float* __restrict__ g_out, float* __restrict__ d_out, Kern K,
-                                                   int tiles_x, int tiles_y, int n_tiles)
-{
-    constexpr int IW = ft_iw(RAD), IH = FT_H + 2 * RAD, LW = FT_W + 2 * RAD;
-    constexpr int NE = IH * LW, NQ = (NE + 255) / 256;
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* in = sm;
-    float* hb = sm + IH * IW;
-    const int tid = threadIdx.x;
-    const int tpi = tiles_x * tiles_y;
-    float pre[NQ];
-    auto fetch = [&](int T) {
-        const int img = T / tpi, rem = T - img * tpi;
-        const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
-        const int ylo = ty * FT_H - RAD, xlo = tx * FT_W - RAD;
-        const bool interior = ylo >= 0 && ylo + IH <= R && xlo >= 0 && xlo + LW <= C;
-        const float* sp = src + img * plane;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int e = tid + 256 * q;
-            if (e < NE) {
-                const int rr = e / LW, cc = e - rr * LW;
-                const int y = interior ? ylo + rr : vo_reflect101(ylo + rr, R);
-                const int x = interior ? xlo + cc : vo_reflect101(xlo + cc, C);
-                pre[q] = sp[(size_t)y * pitch + x];
-            }
-        }
-    };
-    int T = blockIdx.x;
-    if (T < n_tiles) fetch(T);
-    for (; T < n_tiles; T += gridDim.x) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int e = tid + 256 * q;
-            if (e < NE) {
-                const int rr = e / LW, cc = e - rr * LW;
-                in[rr * IW + cc] = pre[q];
-            }
-        }
-        __syncthreads();
-        if (T + (int)gridDim.x < n_tiles) fetch(T + gridDim.x);
-        // ---- row pass ----
-        for (int t = tid; t < IH * (FT_W / FT_V); t += 256) {
-            const int rr = t >> 3, c0 = (t & 7) * FT_V;
-            const float* s = in + rr * IW + c0;
-            float v[FT_V + 2 * RAD];
-#pragma unroll
-            for (int k = 0; k < FT_V + 2 * RAD; ++k) v[k] = s[k];
-#pragma unroll
-            for (int i = 0; i < FT_V; ++i) {
-                float acc = K.k[0] * v[i + RAD];
-#pragma unroll
-                for (int j = 1; j <= RAD; ++j) acc = fmaf(K.k[j], v[i + RAD - j] + v[i + RAD + j], acc);
-                hb[rr * FT_HW + c0 + i] = acc;
-            }
-        }
-        __syncthreads();
-        // ---- column pass + G/DoG stores ----
-        const int img = T / tpi, rem = T - img * tpi;
-        const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
-        const int x0 = tx * FT_W, y0 = ty * FT_H;
-        for (int t = tid; t < FT_W * (FT_H / FT_V); t += 256) {
-            const int c = t & 63, y0l = (t >> 6) * FT_V;
-            const int x = x0 + c;
-            const float* s = hb + y0l * FT_HW + c;
-            float v[FT_V + 2 * RAD];
-#pragma unroll
-            for (int k = 0; k < FT_V + 2 * RAD; ++k) v[k] = s[k * FT_HW];
-            if (x < C) {
-#pragma unroll
-                for (int i = 0; i < FT_V; ++i) {
-                    float acc = K.k[0] * v[i + RAD];
-#pragma unroll
-                    for (int j = 1; j <= RAD; ++j) acc = fmaf(K.k[j], v[i + RAD - j] + v[i + RAD + j], acc);
-                    const int y = y0 + y0l + i;
-                    if (y < R) {
-                        const size_t o = img * dplane + (size_t)y * pitch + x;
-                        g_out[o] = acc;
-                        if (d_out) d_out[o] = acc - in[(y0l + i + RAD) * IW + c + RAD];
-                    }
-                }
-            }
-        }
-        __syncthreads();
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Streaming level blur (MODE 0, compiled radius): one wave per (image, band of
 // TH output rows, strip of 256 columns).  The wave walks the band's TH + 2r
 // input rows top to bottom; each lane owns 4 consecutive columns.
@@ -1597,56 +1500,35 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
                           float* g, float* d, const Kern& K, const ImageSrc& isrc, int in_rows, int in_cols, const char* name)
 {
     const size_t lds = sizeof(float) * ft_lds_floats(K.r);
-    static const int use_pipe = getenv("VO_BLUR_PIPE") ? atoi(getenv("VO_BLUR_PIPE")) : 0;
-    if constexpr (MODE == 0 && RAD > 0) if (!use_pipe) {
-        static const int th_env = getenv("VO_BLUR_TH") ? atoi(getenv("VO_BLUR_TH")) : 128;
-        static const int wave_target = getenv("VO_BLUR_WAVES") ? atoi(getenv("VO_BLUR_WAVES")) : 2048;
-        // band height: a multiple of P, at most th_env, lowered on small octaves until
-        // the launch has ~wave_target waves (2048: 8 per CU; 1024 measured ~1.5 % slower) -- small planes are latency-bound
-        // level blurs of planes at most cpl2_maxc wide use 2 columns per lane (128-column
-        // strips, half the ring registers): more waves and fewer idle lanes at the
-        // narrow octaves, where the kernel is latency-bound rather than HBM-bound
-        static const int cpl2_maxc = getenv("VO_BLUR_CPL2_MAXC") ? atoi(getenv("VO_BLUR_CPL2_MAXC")) : 1400;
+    if constexpr (MODE == 0 && RAD > 0) {
+        // band height: a multiple of P, at most 128 rows, lowered on small octaves until the
+        // launch has ~2048 waves (8 per CU; 1024 measured ~1.5 % slower) -- small planes are
+        // latency-bound.  Level blurs of planes at most 1400 columns wide use 2 columns per
+        // lane (128-column strips, half the ring registers): more waves and fewer idle lanes
+        // at the narrow octaves, where the kernel is latency-bound rather than HBM-bound.
+        constexpr int kMaxTH = 128, kWaveTarget = 2048, kCpl2MaxC = 1400;
         const bool base = name[7] == 'b';
-        const int cpl = (!base && C <= cpl2_maxc) ? 2 : 4;
+        const int cpl = (!base && C <= kCpl2MaxC) ? 2 : 4;
         const int n_strips = (C + 64 * cpl - 1) / (64 * cpl);
         const long rows_total = (long)R * n_strips * grid.z;
-        int TH = (int)std::min<long>(th_env, rows_total / wave_target);
+        int TH = (int)std::min<long>(kMaxTH, rows_total / kWaveTarget);
         TH = std::max(BS_P, TH / BS_P * BS_P);
         if (R >= TH) {
             const int n_bands = (R + TH - 1) / TH;
             const int blocks = n_strips * n_bands * (int)grid.z;
-            static const int cached = getenv("VO_BLUR_CACHED") ? atoi(getenv("VO_BLUR_CACHED")) : 0;
 #define VO_BS_GO(T, CP)                                                                                               \
     VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, T, CP>), dim3(blocks), dim3(64), 0, s, src, plane, dplane, pitch, R, C, g, \
                     K, n_strips, n_bands, TH, isrc, in_rows, in_cols)
             if (base && src == nullptr) VO_BS_GO(5, 4);      // "k_blur_base" from the u8 image (x2 upsample fused)
             else if (base) VO_BS_GO(1, 4);
-            else if (cpl == 2) { if (cached) VO_BS_GO(2, 2); else VO_BS_GO(0, 2); }
-            else if (cached) VO_BS_GO(2, 4);
+            else if (cpl == 2) VO_BS_GO(0, 2);
             else VO_BS_GO(0, 4);
 #undef VO_BS_GO
             return;
         }
     }
-    if (MODE == 0 && RAD > 0) {
-        // persistent grid: as many blocks as can be co-resident, walking all tiles
-        static int per_cu = 0;
-        if (!per_cu) {
-            if (lds > 64 * 1024)
-                hipFuncSetAttribute((const void*)k_blur_pipe<RAD>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_blur_pipe<RAD>, 256, lds);
-            if (per_cu < 1) per_cu = 1;
-        }
-        int dev = 0, cus = 256;
-        hipGetDevice(&dev);
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const int n_tiles = grid.x * grid.y * grid.z;
-        const int blocks = std::min(n_tiles, per_cu * cus);
-        VO_LAUNCH_NAMED(name, k_blur_pipe<RAD>, dim3(blocks), dim3(256), lds, s, src, plane, dplane, pitch, R, C, g, d, K,
-                        (int)grid.x, (int)grid.y, n_tiles);
-        return;
-    }
+    // generic tiled form: kernel radii without a streaming instantiation, planes shorter than
+    // one band (tiny images; GPU edge tests), and the non-upsampled / split octave-0 base
     if (lds > 64 * 1024) {
         static bool once = false;
         if (!once) {
@@ -1712,10 +1594,9 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
         if (o == 0) {
             Kern K0 = make_kern(py, 0);
             const int rows = p.upsample ? R / 2 : R, cols = p.upsample ? C / 2 : C;
-            static const bool split = getenv("VO_BASE_SPLIT") != nullptr || getenv("VO_BLUR_PIPE") != nullptr;
             const int r0 = K0.r;
             const bool stream_r = r0 == 5 || r0 == 6 || r0 == 8 || r0 == 10 || r0 == 13;
-            if (p.upsample && stream_r && R >= 64 && !split) {
+            if (p.upsample && stream_r && R >= 64) {
                 // level-0 blur straight from the u8 image, x2 upsample formed while staging rows
                 launch_blur<0>(gf, s, nullptr, 0, py.istride, g.pitch, R, C, A + g.g_off[0], nullptr, K0, src, rows, cols,
                                "k_blur_base");
@@ -1757,16 +1638,11 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
     }
 }
 
-// grid of the wave-per-keypoint kernels (grid-stride over the flat keypoint space)
-static int feature_grid(const char* env)
-{
-    // 32768 one-wave workgroups (~7 keypoints each at 64 frames x ~1.8k): shorter tail than
-    // 8192 (k_desc 2.25 -> 2.05 ms, k_orient 0.77 -> 0.67 ms isolated) and workgroups turn over
-    // often enough for the scale-space stream's blurs to get slots while they run
-    const char* v = getenv(env);
-    const int g = v ? atoi(v) : 32768;
-    return g > 0 ? g : 32768;
-}
+// grid of the wave-per-keypoint kernels (grid-stride over the flat keypoint space):
+// 32768 one-wave workgroups (~7 keypoints each at 64 frames x ~1.8k): shorter tail than
+// 8192 (k_desc 2.25 -> 2.05 ms, k_orient 0.77 -> 0.67 ms isolated) and workgroups turn over
+// often enough for the scale-space stream's blurs to get slots while they run
+constexpr int kFeatureGrid = 32768;
 
 void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
                            const Pyramid* d_py)
@@ -1778,13 +1654,13 @@ void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const v
     VO_LAUNCH(k_seg_emit, gs, dim3(256), 0, s, d_py, b.mask, (const uint32_t*)b.woff, b.cand, b.cand_cap);
     VO_LAUNCH(k_refine, dim3(512), dim3(256), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.cand_cap, n_img,
               p.contrast_threshold, p.edge_threshold, p.sigma);
-    VO_LAUNCH_NAMED("k_orient", (k_orient<37>), dim3(feature_grid("VO_ORIENT_GRID")), dim3(64), 0, s, d_py, A, b.n_cand,
+    VO_LAUNCH_NAMED("k_orient", (k_orient<37>), dim3(kFeatureGrid), dim3(64), 0, s, d_py, A, b.n_cand,
                     b.cout, b.cand_cap, n_img);
     VO_LAUNCH(k_scan_cands, dim3(n_img), dim3(1024), 0, s, b.cout, b.n_cand, b.koff, b.n_kp, b.cand_cap);
     VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, b.n_cand, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
                        n_img, p.upsample);
     // 4 histogram copies: 2 -> +4 %, 8 -> +33 % k_desc time (MI355X)
-    VO_LAUNCH_NAMED("k_desc", (k_desc<4>), dim3(feature_grid("VO_DESC_GRID")), dim3(64), 0, s, d_py, A, b.kpi, b.n_kp, b.desc,
+    VO_LAUNCH_NAMED("k_desc", (k_desc<4>), dim3(kFeatureGrid), dim3(64), 0, s, d_py, A, b.kpi, b.n_kp, b.desc,
                     b.meta, b.kp_cap, n_img);
 }
 

@@ -121,6 +121,10 @@ struct vo_ctx {
     bool have_features = false;
     double pose[16];
     std::vector<double> landmarks;
+    // camera-frame landmark rows (vo_set_landmark_frame(ctx, 1)): sharded sequences
+    int lm_camera = 0;
+    std::vector<float> lm_X;
+    std::vector<uint8_t> lm_keep;
 };
 
 static std::string g_create_err;
@@ -150,7 +154,7 @@ void vo_default_sift_params(vo_sift_params* p)
 void vo_default_match_params(vo_match_params* p) { p->match_threshold = 1.0f; p->max_ratio = 0.6f; }
 void vo_default_ransac_params(vo_ransac_params* p)
 {
-    p->max_num_trials = 2048; p->confidence = 99.0; p->max_reprojection_error = 1.0; p->seed = 0x5EED;
+    p->max_num_trials = 1000; p->confidence = 99.0; p->max_reprojection_error = 1.0; p->seed = 0x5EED;
 }
 
 const char* vo_last_error(const vo_ctx* c) { return c ? c->err.c_str() : g_create_err.c_str(); }
@@ -418,6 +422,7 @@ int vo_sift(vo_ctx* c, const uint8_t* img, int rows, int cols, int ld, vo_keypoi
     HIPC(c, hipMemcpy2DAsync(c->d_img, cols, img, ld, cols, rows, hipMemcpyHostToDevice, c->stream));
     ImageSrc src{c->d_img, c->d_img, (size_t)rows * cols, cols, 0};
     sift_enqueue(c->py, c->sb, src, 1, c->sp, c->stream, c->d_py);
+    c->last_set = 0;                                   // vo_fetch_* now read this result (set 0)
     int n = 0;
     HIPC(c, hipMemcpyAsync(&n, c->sb.n_kp, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     int rc = finish(c);
@@ -755,10 +760,15 @@ static int collect_batch(vo_ctx* c, vo_step_out* outs, int capacity, int* n_out)
             }
             const int r = (int)keep[f].size();
             o.n_landmarks = r;
-            size_t base = c->landmarks.size();
-            c->landmarks.resize(base + (size_t)r * 3, 0.0);
-            for (int m = 0; m < r; ++m)
-                if (keep[f][m]) lm_world(c->pose, &X[f][(size_t)m * 3], &c->landmarks[base + (size_t)m * 3]);
+            if (c->lm_camera) {
+                c->lm_X.insert(c->lm_X.end(), X[f].begin(), X[f].end());
+                c->lm_keep.insert(c->lm_keep.end(), keep[f].begin(), keep[f].end());
+            } else {
+                size_t base = c->landmarks.size();
+                c->landmarks.resize(base + (size_t)r * 3, 0.0);
+                for (int m = 0; m < r; ++m)
+                    if (keep[f][m]) lm_world(c->pose, &X[f][(size_t)m * 3], &c->landmarks[base + (size_t)m * 3]);
+            }
         }
         memcpy(o.pose, c->pose, sizeof(c->pose));
     }
@@ -873,6 +883,39 @@ int vo_get_landmarks(vo_ctx* c, double* out, int capacity, int* rows)
     return r > capacity && out ? fail(c, VO_ERR_CAPACITY, "vo_get_landmarks: %d rows exceed capacity %d", r, capacity) : VO_OK;
 }
 
+int vo_set_landmark_frame(vo_ctx* c, int camera)
+{
+    if (!c || (camera != 0 && camera != 1)) return fail(c, VO_ERR_ARG, "vo_set_landmark_frame: mode must be 0 (world) or 1 (camera)");
+    if (!c->pending.empty()) return fail(c, VO_ERR_STATE, "vo_set_landmark_frame: batches pending");
+    c->lm_camera = camera;
+    c->landmarks.clear();
+    c->lm_X.clear();
+    c->lm_keep.clear();
+    return VO_OK;
+}
+
+int vo_get_landmark_rows(vo_ctx* c, float* X, uint8_t* keep, int capacity, int* rows)
+{
+    if (!c || capacity < 0) return fail(c, VO_ERR_ARG, "vo_get_landmark_rows: bad arguments");
+    if (!c->lm_camera) return fail(c, VO_ERR_STATE, "vo_get_landmark_rows: context keeps world rows (vo_set_landmark_frame(ctx, 1) first)");
+    const int r = (int)c->lm_keep.size();
+    if (rows) *rows = r;
+    const int m = std::min(r, capacity);
+    if (X && m > 0) memcpy(X, c->lm_X.data(), sizeof(float) * 3 * m);
+    if (keep && m > 0) memcpy(keep, c->lm_keep.data(), m);
+    return r > capacity && (X || keep) ? fail(c, VO_ERR_CAPACITY, "vo_get_landmark_rows: %d rows exceed capacity %d", r, capacity) : VO_OK;
+}
+
+int vo_landmarks_to_world(const double pose[16], const float* X, const uint8_t* keep, int n, double* out)
+{
+    if (!pose || n < 0 || (n > 0 && (!X || !keep || !out))) return VO_ERR_ARG;
+    for (int m = 0; m < n; ++m) {
+        if (keep[m]) lm_world(pose, X + (size_t)m * 3, out + (size_t)m * 3);
+        else out[3 * m] = out[3 * m + 1] = out[3 * m + 2] = 0.0;
+    }
+    return VO_OK;
+}
+
 int vo_reset(vo_ctx* c)
 {
     if (!c) return VO_ERR_ARG;
@@ -888,6 +931,8 @@ int vo_reset(vo_ctx* c)
     c->frame_index = 0;
     memcpy(c->pose, I4, sizeof(I4));
     c->landmarks.clear();
+    c->lm_X.clear();
+    c->lm_keep.clear();
     HIPC(c, hipMemset(c->d_pair_n + c->max_batch, 0, sizeof(int)));
     HIPC(c, hipMemset(c->aux.pair_n + c->max_batch, 0, sizeof(int)));
     return VO_OK;
@@ -920,6 +965,7 @@ int vo_track(vo_ctx* c, const uint8_t* old_l, const uint8_t* old_r, int n_old, c
     if (n_old > K || n_cl > K || n_cr > K) return fail(c, VO_ERR_CAPACITY, "vo_track: more rows than max_keypoints");
     BEGIN_CALL(c);
     c->have_features = false;
+    c->last_set = 0;                                   // set 0's descriptor slots are overwritten
     int rc;
     if ((rc = upload_desc(c, 2 * M, old_l, n_old))) return rc;
     if ((rc = upload_desc(c, 2 * M + 1, old_r, n_old))) return rc;

@@ -215,10 +215,14 @@ def _pipelined(ctx, batches, dev, on_collect=None) -> list:
         if on_collect is not None:
             on_collect(b0, L, outs)
     for b0, L, R in batches:
-        dl = torch.from_numpy(L).pin_memory().to(dev, non_blocking=True)
-        dr = torch.from_numpy(R).pin_memory().to(dev, non_blocking=True)
-        torch.cuda.current_stream(dev).synchronize()         # inputs ready before the submit
-        ctx.step_submit_dev(dl.data_ptr(), dr.data_ptr(), L.shape[0])
+        if isinstance(L, torch.Tensor):                       # device-resident frames (ready at the call)
+            dl, dr = L.contiguous(), R.contiguous()
+            L = L.cpu().numpy() if on_collect is not None else None
+        else:
+            dl = torch.from_numpy(L).pin_memory().to(dev, non_blocking=True)
+            dr = torch.from_numpy(R).pin_memory().to(dev, non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()     # inputs ready before the submit
+        ctx.step_submit_dev(dl.data_ptr(), dr.data_ptr(), dl.shape[0])
         inflight.append((dl, dr, b0, L if on_collect is not None else None))
         if ctx.steps_pending() == 2:
             collect()
@@ -227,7 +231,7 @@ def _pipelined(ctx, batches, dev, on_collect=None) -> list:
     return outs
 
 
-def run(seq: KittiSequence, batch: int = 16, stop: int | None = None, device: int = 0, ctx=None,
+def run(seq: KittiSequence, batch: int = 16, stop: int | None = None, device: int | None = None, ctx=None,
         viz_dir: str | os.PathLike | None = None, viz_every: int = 100):
     """The VO.m loop over a KITTI sequence through libvo: frames in batches of `batch`
     (pipelined vo_step_submit_dev / vo_step_collect, tracking carried across batches), H2D
@@ -238,6 +242,7 @@ def run(seq: KittiSequence, batch: int = 16, stop: int | None = None, device: in
     landmarks [L, 3])."""
     import torch
     from . import vo
+    device = _local_device() if device is None else device
     own = ctx is None
     if own:
         ctx = vo.Context(seq.rows, seq.cols, batch, device=device, calib=vo.calib_from(seq.P1, seq.P2))
@@ -261,38 +266,92 @@ def run(seq: KittiSequence, batch: int = 16, stop: int | None = None, device: in
     return poses, outs, lm
 
 
-def run_shard(seq: KittiSequence, rank: int, world: int, batch: int = 16, device: int = 0,
-              stop: int | None = None) -> np.ndarray:
+def device_batches(dL, dR, batch: int, start: int = 0, stop: int | None = None):
+    """Batches of device-resident frames (torch uint8 tensors [n, H, W] on the GPU), in the
+    (first_frame, L, R) form `_pipelined` takes; no copies."""
+    stop = dL.shape[0] if stop is None else min(stop, dL.shape[0])
+    for b0 in range(start, stop, batch):
+        yield b0, dL[b0:min(b0 + batch, stop)], dR[b0:min(b0 + batch, stop)]
+
+
+def _local_device() -> int:
+    """This process's GPU: LOCAL_RANK under torchrun (one process per GPU), else 0."""
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def run_shard(seq, rank: int, world: int, batch: int = 16, device: int | None = None,
+              stop: int | None = None, ctx=None):
     """One rank's part of a frame-sharded run (`sharding.py`): the block
-    [start, end) of frames plus a one-frame halo, MSAC keyed by the global frame index.
-    Returns the block's relative poses [end - start, 4, 4] (frame 0's is the identity)."""
+    [start, end) of frames plus a one-frame halo, MSAC keyed by the global frame index,
+    landmark rows kept in the camera frame.  `seq` is a KittiSequence (PNG frames) or a
+    (L, R) pair of device tensors [n, H, W] holding the whole sequence (or at least
+    frames [halo, end)).  Returns (outs: the block's STEP_DTYPE records [end - start],
+    X [L, 3] float32, keep [L] bool: the block's camera-frame landmark rows)."""
     import torch
     from . import sharding, vo
-    n = len(seq) if stop is None else min(stop, len(seq))
+    device = _local_device() if device is None else device
+    on_device = isinstance(seq, tuple)
+    n_all = seq[0].shape[0] if on_device else len(seq)
+    n = n_all if stop is None else min(stop, n_all)
     s, e = sharding.shard_range(n, world, rank)
     h = sharding.halo_start(s)
-    ctx = vo.Context(seq.rows, seq.cols, batch, device=device, calib=vo.calib_from(seq.P1, seq.P2))
+    own = ctx is None
+    if own:
+        rows, cols = (seq[0].shape[1], seq[0].shape[2]) if on_device else (seq.rows, seq.cols)
+        ctx = vo.Context(rows, cols, batch, device=device, calib=vo.calib_from(seq_calib(seq)[0], seq_calib(seq)[1]))
     ctx.reset()
+    ctx.set_landmark_frame(True)
     ctx.set_frame_index(h)
-    outs = _pipelined(ctx, seq.batches(batch, h, e), torch.device("cuda", device))
-    ctx.close()
-    outs = np.concatenate(outs)
-    return outs["rel_pose"][s - h:]
+    src = device_batches(seq[0], seq[1], batch, h, e) if on_device else seq.batches(batch, h, e)
+    outs = _pipelined(ctx, src, torch.device("cuda", device))
+    X, keep = ctx.get_landmark_rows()
+    if own:
+        ctx.close()
+    outs = np.concatenate(outs) if outs else np.zeros(0, vo.STEP_DTYPE)
+    return outs[s - h:], X, keep
 
 
-def run_distributed(seq: KittiSequence, batch: int = 16, device: int = 0, stop: int | None = None,
-                    group=None) -> np.ndarray:
+def seq_calib(seq):
+    """(P1, P2) of a KittiSequence, or of a device-frame tuple (L, R[, P1, P2])."""
+    if isinstance(seq, tuple):
+        if len(seq) >= 4:
+            return seq[2], seq[3]
+        from .synthetic import KITTI00_P0, KITTI00_P1
+        return KITTI00_P0, KITTI00_P1
+    return seq.P1, seq.P2
+
+
+def assemble(steps: dict, X: np.ndarray, keep: np.ndarray, to_world=None):
+    """World poses (VO.m:130 chain, failed frames hold the pose) and the world landmark map
+    (CreateLandmarksFromFeatures.m:17 per frame, after the chain) from gathered frame records
+    and camera-frame landmark rows."""
+    from . import sharding
+    if to_world is None:
+        from .vo import landmarks_to_world as to_world
+    poses = sharding.chain(steps["rel_pose"], status=steps["status"])
+    lm = sharding.world_landmarks(poses, steps["n_landmarks"], X, keep, to_world)
+    return poses, lm
+
+
+def run_distributed(seq, batch: int = 16, device: int | None = None, stop: int | None = None,
+                    group=None):
     """Frame-sharded run over a torch.distributed group (one process per GPU; RCCL over
-    xGMI with the nccl backend): every rank runs its block (`run_shard`), one all-gather
-    of 16 doubles per frame collects the relative poses, and the world-pose chain is the
-    host product of `VO.m:130`.  Returns world poses [n, 4, 4] on every rank, equal bit for
-    bit to a single-process run.  (The landmark map needs the world chain before its
-    transform step; use `run` for it.)"""
+    xGMI with the nccl backend): every rank runs its block (`run_shard`), one all-gather of
+    the per-frame records (relative pose, status, counts) and one of the camera-frame
+    landmark rows, then the world-pose chain (host product of `VO.m:130`) and the landmark
+    world transform (`CreateLandmarksFromFeatures.m:17`).  Returns (world poses [n, 4, 4],
+    gathered per-frame records, landmarks [L, 3]) on every rank, equal bit for bit to a
+    single-process run."""
     import torch
     import torch.distributed as dist
     from . import sharding
-    n = len(seq) if stop is None else min(stop, len(seq))
+    device = _local_device() if device is None else device
+    n_all = seq[0].shape[0] if isinstance(seq, tuple) else len(seq)
+    n = n_all if stop is None else min(stop, n_all)
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    rel = run_shard(seq, rank, world, batch, device, n)
+    outs, X, keep = run_shard(seq, rank, world, batch, device, n)
     dev = torch.device("cuda", device) if dist.get_backend(group) == "nccl" else None
-    return sharding.chain(sharding.gather_rel_poses(rel, n, group=group, device=dev))
+    steps = sharding.gather_steps(outs, n, group=group, device=dev)
+    Xg, kg = sharding.gather_landmark_rows(X, keep, group=group, device=dev)
+    poses, lm = assemble(steps, Xg, kg)
+    return poses, steps, lm

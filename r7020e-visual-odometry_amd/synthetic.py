@@ -34,6 +34,9 @@ SEED_BASE = 0x5EED0000
 # BASELINE configs[4]: 1920x1080, ~8k keypoints per image.  At the default 16 px per texture
 # cell the oracle finds ~6.8k; 14.5 px per cell gives 8k +- 10 % (tests/test_gpu_large.py).
 LARGE_ROWS, LARGE_COLS, LARGE_PX_PER_CELL = 1080, 1920, 14.5
+# BASELINE configs[1]: ~2k keypoints per 1242x375 image.  16 px per cell gives the oracle ~1790,
+# 15 px ~2020 (16 pairs), inside SURVEY §8(d)'s 2000 +- 200.
+BENCH_PX_PER_CELL = 15.0
 
 
 @dataclass

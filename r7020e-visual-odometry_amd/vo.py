@@ -91,6 +91,7 @@ EXPORTS = [
     "vo_steps_pending", "vo_fetch_tracks", "vo_get_landmarks", "vo_reset",
     "vo_sift_match_batch_dev", "vo_fetch_keypoints", "vo_fetch_stereo_pairs", "vo_fetch_gaussian", "vo_stream", "vo_set_profiling",
     "vo_kernel_times", "vo_set_frame_index", "vo_set_concurrency",
+    "vo_set_landmark_frame", "vo_get_landmark_rows", "vo_landmarks_to_world",
 ]
 
 _lib = None
@@ -153,6 +154,9 @@ def load_library(path: str | os.PathLike | None = None):
     L.vo_stream.restype = vp
     L.vo_set_profiling.argtypes = [vp, C.c_int]
     L.vo_set_concurrency.argtypes = [vp, C.c_int]
+    L.vo_set_landmark_frame.argtypes = [vp, C.c_int]
+    L.vo_get_landmark_rows.argtypes = [vp, P(C.c_float), P(C.c_uint8), C.c_int, P(C.c_int)]
+    L.vo_landmarks_to_world.argtypes = [P(C.c_double), P(C.c_float), P(C.c_uint8), C.c_int, P(C.c_double)]
     L.vo_kernel_times.argtypes = [vp, P(C.c_char_p), P(C.c_double), P(C.c_int), C.c_int, P(C.c_int)]
     _lib = L
     return L
@@ -387,6 +391,20 @@ class Context:
         self._check(self.lib.vo_get_landmarks(self.h, _p(out, C.c_double), rows.value, C.byref(rows)))
         return out[: rows.value].copy()
 
+    def set_landmark_frame(self, camera: bool):
+        """Keep landmark rows in the camera frame (sharded sequences) instead of the world."""
+        self._check(self.lib.vo_set_landmark_frame(self.h, 1 if camera else 0))
+
+    def get_landmark_rows(self):
+        """Camera-frame landmark rows appended so far -> (X [L, 3] float32, keep [L] bool)."""
+        rows = C.c_int(0)
+        self._check(self.lib.vo_get_landmark_rows(self.h, None, None, 0, C.byref(rows)))
+        X = np.zeros((max(rows.value, 1), 3), np.float32)
+        keep = np.zeros(max(rows.value, 1), np.uint8)
+        self._check(self.lib.vo_get_landmark_rows(self.h, _p(X, C.c_float), _p(keep, C.c_uint8), rows.value,
+                                                  C.byref(rows)))
+        return X[: rows.value].copy(), keep[: rows.value].astype(bool)
+
     def reset(self):
         self._check(self.lib.vo_reset(self.h))
 
@@ -416,6 +434,20 @@ class Context:
 
     def stream(self) -> int:
         return self.lib.vo_stream(self.h) or 0
+
+
+def landmarks_to_world(pose, X, keep) -> np.ndarray:
+    """CreateLandmarksFromFeatures.m:17 on camera-frame rows (vo_landmarks_to_world): rows with
+    keep=False stay the reference's zero rows."""
+    pose = np.ascontiguousarray(pose, np.float64).reshape(4, 4)
+    X = np.ascontiguousarray(X, np.float32).reshape(-1, 3)
+    k = np.ascontiguousarray(keep, np.uint8).reshape(-1)
+    out = np.zeros((X.shape[0], 3))
+    rc = load_library().vo_landmarks_to_world(_p(pose, C.c_double), _p(X, C.c_float), _p(k, C.c_uint8), X.shape[0],
+                                               _p(out, C.c_double))
+    if rc != VO_OK:
+        raise VOError(rc, "vo_landmarks_to_world: bad arguments")
+    return out
 
 
 # ---------------------------------------------------------------------------

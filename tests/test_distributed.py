@@ -1,14 +1,17 @@
-"""Multi-rank path on CPU (gloo, world_size 2): the sequence is block-sharded
-with a one-frame halo, each rank runs its frames (here through the CPU oracle,
-standing in for its GPU), relative poses are all-gathered and chained, and the
-result equals the single-process run bit for bit (MSAC keys are global frame
-indices)."""
+"""Multi-rank path on CPU (gloo): a sequence is block-sharded with a one-frame halo,
+each rank runs its frames (through the CPU oracle, standing in for its GPU: these
+ranks are libvo-free), the per-frame records and the camera-frame landmark rows are
+all-gathered, the relative poses are chained and the landmark rows moved to the world
+with their frame's chained pose (CreateLandmarksFromFeatures.m:17).
+World poses AND the landmark map equal the single-process run bit for bit (MSAC keys
+are global frame indices)."""
 import os
 import socket
 import sys
 from pathlib import Path
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -22,42 +25,81 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, result_q):
+def _worker(rank, world, port, path, result_q):
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "oracle"))
+    import torch
     import torch.distributed as dist
     import vo_amd  # noqa: F401
-    from r7020e_visual_odometry_amd import sharding
+    from r7020e_visual_odometry_amd import sharding, kitti
     import oracle
+    torch.set_num_threads(1)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    z = np.load(ROOT / "tests" / "golden" / "sequence.npz")
+    z = np.load(path)
     L, R = z["L"], z["R"]
     n = len(L)
     s, e = sharding.shard_range(n, world, rank)
     h = sharding.halo_start(s)
-    outs, _ = oracle.run_sequence(L[h:e], R[h:e], z["P1"], z["P2"], key0=h)
-    rel_local = outs["rel_pose"][s - h:]          # drop the halo frame
-    rel = sharding.gather_rel_poses(rel_local, n)
-    poses = sharding.chain(rel)
+    outs, (X, keep) = oracle.run_sequence(L[h:e], R[h:e], z["P1"], z["P2"], key0=h, camera_rows=True)
+    outs = outs[s - h:]                                  # drop the halo frame
+    steps = sharding.gather_steps(outs, n)
+    Xg, kg = sharding.gather_landmark_rows(X, keep)
+    poses, lm = kitti.assemble(steps, Xg, kg, to_world=oracle.landmarks_to_world)
     if rank == 0:
-        result_q.put((rel, poses))
+        result_q.put((steps, poses, lm))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_sharded_sequence_equals_single_process():
-    z = np.load(ROOT / "tests" / "golden" / "sequence.npz")
+def _run(world, path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(path), q)) for r in range(world)]
     for p in procs:
         p.start()
-    rel, poses = q.get(timeout=300)
+    res = q.get(timeout=600)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert np.array_equal(rel, z["out_rel_pose"])
-    assert np.array_equal(poses, z["out_pose"])
+    return res
+
+
+def _check(res, ref_outs, ref_lm):
+    steps, poses, lm = res
+    assert np.array_equal(steps["rel_pose"], ref_outs["rel_pose"])
+    for k in ("status", "n_left", "n_right", "n_stereo", "n_tracked", "n_inliers", "n_landmarks"):
+        assert np.array_equal(steps[k], ref_outs[k]), k
+    assert np.array_equal(poses, ref_outs["pose"])
+    assert lm.shape == ref_lm.shape and np.array_equal(lm, ref_lm)
+
+
+def test_two_rank_sharded_golden_sequence_equals_single_process(tmp_path):
+    z = np.load(ROOT / "tests" / "golden" / "sequence.npz")
+    ref = {k[4:]: z[k] for k in z.files if k.startswith("out_")}
+    _check(_run(2, ROOT / "tests" / "golden" / "sequence.npz"), ref, z["landmarks"])
+
+
+@pytest.fixture(scope="module")
+def street_seq(tmp_path_factory, oracle):
+    """6 frames along KITTI-00's ground truth (frames 1500-1505), rendered at half size."""
+    import torch
+    from r7020e_visual_odometry_amd import street, synthetic as syn
+    torch.set_num_threads(4)
+    gt = street.kitti00_gt()
+    P0, P1 = syn.calib(0.5)
+    w = street.kitti00_world()
+    L, R = street.render_frames(w, gt, range(1500, 1506), P0, P1, rows=188, cols=620, chunk=6)
+    path = tmp_path_factory.mktemp("street") / "seq.npz"
+    np.savez(path, L=L.numpy(), R=R.numpy(), P1=P0, P2=P1)
+    outs, lm = oracle.run_sequence(L.numpy(), R.numpy(), P0, P1)
+    return path, outs, lm
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_street_sequence_poses_and_landmarks_equal_single_process(street_seq, world):
+    path, outs, lm = street_seq
+    assert (outs["status"][1:] == 0).all() and len(lm) > 100
+    _check(_run(world, path), outs, lm)
