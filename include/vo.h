@@ -134,10 +134,25 @@ const char* vo_last_error(const vo_ctx* ctx);
 int vo_sift(vo_ctx* ctx, const uint8_t* img, int rows, int cols, int ld,
             vo_keypoint* kps, uint8_t* desc, int capacity, int* n_out);
 
+/* The same for an image in MATLAB's own storage: col_major = 1 means pixel (r, c) at
+ * img[c * ld + r] (ld >= rows; a MEX gateway passes mxGetUint8s(I) with ld = rows, no
+ * transpose on the host; the device transposes).  col_major = 0 is vo_sift. */
+int vo_sift_ex(vo_ctx* ctx, const uint8_t* img, int rows, int cols, int ld, int col_major,
+               vo_keypoint* kps, uint8_t* desc, int capacity, int* n_out);
+
 /* matchFeatures(F1, F2) on SIFT descriptors (uint8 rows of 128).
  * pairs[capacity][2] 1-based; *n_pairs = matches found. */
 int vo_match(vo_ctx* ctx, const uint8_t* F1, int n1, const uint8_t* F2, int n2,
              uint32_t* pairs, int capacity, int* n_pairs);
+
+/* matchFeatures(F1, F2) on single-precision descriptor matrices exactly as MATLAB holds
+ * extractFeatures' output (VO.m:83-87): n x 128 single with integer values 0..255.
+ * col_major = 1: element (i, k) at F[i + k * ld] (MATLAB storage; ld >= n), so a MEX gateway
+ * passes mxGetSingles(prhs[k]) with ld = n and no transpose or conversion; col_major = 0:
+ * F[i * ld + k] (ld >= 128).  The matrices are copied to the device as they lie and packed to
+ * u8 rows there.  Non-integer or out-of-range values -> VO_ERR_ARG.  Same results as vo_match. */
+int vo_match_f32(vo_ctx* ctx, const float* F1, int n1, int ld1, const float* F2, int n2, int ld2,
+                 int col_major, uint32_t* pairs, int capacity, int* n_pairs);
 
 /* find_remaining_points (VO.m:280-334) on device.  old = previous frame's
  * stereo-aligned set (n_old rows, left/right row-aligned); cur = current
@@ -194,6 +209,10 @@ int vo_step(vo_ctx* ctx, const uint8_t* left, const uint8_t* right, int ld, vo_s
  * chain is sequential (host).  Equivalent to B calls of vo_step. */
 int vo_step_batch(vo_ctx* ctx, const uint8_t* lefts, const uint8_t* rights, int ld, int B,
                   vo_step_out* outs);
+/* Same with a storage-order flag: col_major = 1 takes B column-major (MATLAB) frames, frame n
+ * at lefts + n * ld * cols, pixel (r, c) at [c * ld + r]. */
+int vo_step_batch_ex(vo_ctx* ctx, const uint8_t* lefts, const uint8_t* rights, int ld, int col_major, int B,
+                     vo_step_out* outs);
 /* Same, inputs already in device memory (tightly packed rows*cols each). */
 int vo_step_batch_dev(vo_ctx* ctx, const uint8_t* d_lefts, const uint8_t* d_rights, int B,
                       vo_step_out* outs);

@@ -373,6 +373,34 @@ void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, con
     VO_LAUNCH(k_match_compact, dim3(n_jobs), dim3(1024), 0, s, d_jobs, (const int*)b.res, b.row_cap);
 }
 
+// single-precision descriptor matrix (MATLAB's extractFeatures output: n x 128 single, integer
+// values 0..255) -> packed u8 rows.  col_major: element (i, k) at F[i + k * ld] (MATLAB's own
+// layout, so a MEX gateway passes mxGetSingles() without a copy); else F[i * ld + k].  One
+// thread per element, the row index fastest for column-major input (coalesced reads).  A value
+// that is not an integer in [0, 255] raises *bad.
+__global__ __launch_bounds__(256) void k_pack_f32_desc(const float* __restrict__ F, int n, int ld, int col_major,
+                                                       uint8_t* __restrict__ out, int* __restrict__ bad)
+{
+    const long total = (long)n * VO_DESC_LEN;
+    for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+        int i, k;
+        float v;
+        if (col_major) { i = (int)(t % n); k = (int)(t / n); v = F[(size_t)k * ld + i]; }
+        else { i = (int)(t / VO_DESC_LEN); k = (int)(t % VO_DESC_LEN); v = F[(size_t)i * ld + k]; }
+        const bool ok = v >= 0.0f && v <= 255.0f && v == rintf(v);
+        out[(size_t)i * VO_DESC_LEN + k] = ok ? (uint8_t)v : 0;
+        if (!ok) *bad = 1;
+    }
+}
+
+void pack_f32_desc_launch(const float* F, int n, int ld, int col_major, uint8_t* out, int* bad, hipStream_t s)
+{
+    if (n <= 0) return;
+    long total = (long)n * VO_DESC_LEN;
+    int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+    VO_LAUNCH(k_pack_f32_desc, dim3(blocks), dim3(256), 0, s, F, n, ld, col_major, out, bad);
+}
+
 void desc_meta_launch(const uint8_t* desc, DescMeta* meta, int n, hipStream_t s)
 {
     if (n <= 0) return;

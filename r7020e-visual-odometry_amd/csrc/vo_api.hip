@@ -95,10 +95,14 @@ struct vo_ctx {
     int* d_pair_j = nullptr;
     int* d_pair_n = nullptr;         // [slots]
     uint8_t* d_img = nullptr;        // image staging [2*max_batch][rows*cols]
+    uint8_t* d_cm = nullptr;         // column-major (MATLAB) image staging, allocated on first use
+    size_t cm_cap = 0;
     // vo_match staging
     uint8_t* d_fd[2] = {nullptr, nullptr};
     DescMeta* d_fm[2] = {nullptr, nullptr};
     int* d_fn = nullptr;             // [2]
+    float* d_ff[2] = {nullptr, nullptr};   // vo_match_f32 staging (single descriptors as MATLAB holds them)
+    int* d_bad = nullptr;
     int* d_mi = nullptr; int* d_mj = nullptr; int* d_mn = nullptr;
     GeomBuffers gb;
     // Pipelined full path (vo_step_submit_dev / vo_step_collect): batch n uses buffer set
@@ -198,7 +202,8 @@ static void destroy_buffers(vo_ctx* c)
     }
     geom_free(c->gb);
     hipFree(c->d_py); hipFree(c->d_jobs); hipFree(c->d_pair_i); hipFree(c->d_pair_j); hipFree(c->d_pair_n);
-    hipFree(c->d_img); hipFree(c->d_fd[0]); hipFree(c->d_fd[1]); hipFree(c->d_fm[0]); hipFree(c->d_fm[1]);
+    hipFree(c->d_img); hipFree(c->d_cm); hipFree(c->d_fd[0]); hipFree(c->d_fd[1]); hipFree(c->d_fm[0]); hipFree(c->d_fm[1]);
+    hipFree(c->d_ff[0]); hipFree(c->d_ff[1]); hipFree(c->d_bad);
     hipFree(c->d_fn); hipFree(c->d_mi); hipFree(c->d_mj); hipFree(c->d_mn);
 }
 
@@ -269,8 +274,10 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
     for (int k = 0; k < 2; ++k) {
         if ((e = hipMalloc((void**)&c->d_fd[k], (size_t)kp_cap * VO_DESC_LEN)) != hipSuccess) return bail("staging", e);
         if ((e = hipMalloc((void**)&c->d_fm[k], sizeof(DescMeta) * kp_cap)) != hipSuccess) return bail("staging", e);
+        if ((e = hipMalloc((void**)&c->d_ff[k], sizeof(float) * kp_cap * VO_DESC_LEN)) != hipSuccess) return bail("staging", e);
     }
     if ((e = hipMalloc((void**)&c->d_fn, sizeof(int) * 2)) != hipSuccess) return bail("staging", e);
+    if ((e = hipMalloc((void**)&c->d_bad, sizeof(int))) != hipSuccess) return bail("staging", e);
     if ((e = hipMalloc((void**)&c->d_mi, sizeof(int) * kp_cap)) != hipSuccess) return bail("staging", e);
     if ((e = hipMalloc((void**)&c->d_mj, sizeof(int) * kp_cap)) != hipSuccess) return bail("staging", e);
     if ((e = hipMalloc((void**)&c->d_mn, sizeof(int))) != hipSuccess) return bail("staging", e);
@@ -414,12 +421,60 @@ static int begin_call(vo_ctx* c, bool quiesce = true, bool step = false)
 }
 #define BEGIN_CALL(...) do { int rc_ = begin_call(__VA_ARGS__); if (rc_) return rc_; } while (0)
 
-int vo_sift(vo_ctx* c, const uint8_t* img, int rows, int cols, int ld, vo_keypoint* kps, uint8_t* desc, int capacity,
-            int* n_out)
+// MATLAB images are column-major: pixel (r, c) of image n at src[n * ld * cols + c * ld + r]
+// (ld >= rows).  32 x 32 LDS tile transpose into tightly packed row-major frames.
+__global__ __launch_bounds__(256) void k_cm_to_rm_u8(const uint8_t* __restrict__ src, int ld, int rows, int cols,
+                                                     uint8_t* __restrict__ dst)
 {
-    if (!c || !img || rows != c->rows || cols != c->cols || ld < cols) return fail(c, VO_ERR_ARG, "vo_sift: bad arguments");
+    __shared__ uint8_t t[32][33];
+    const int n = blockIdx.z, r0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+    const uint8_t* s = src + (size_t)n * ld * cols;
+    uint8_t* d = dst + (size_t)n * rows * cols;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int k = ty; k < 32; k += 8) {
+        const int c = c0 + k, r = r0 + tx;                  // lanes walk a source column (contiguous)
+        if (c < cols && r < rows) t[k][tx] = s[(size_t)c * ld + r];
+    }
+    __syncthreads();
+    for (int k = ty; k < 32; k += 8) {
+        const int r = r0 + k, c = c0 + tx;                  // lanes walk a destination row
+        if (r < rows && c < cols) d[(size_t)r * cols + c] = t[tx][k];
+    }
+}
+
+// host images -> tightly packed row-major device frames at dst (n frames).  col_major: the
+// buffer as MATLAB holds it (copied as it lies into the context's column-major staging, then
+// transposed on the device).
+static int stage_images(vo_ctx* c, const uint8_t* img, int ld, int col_major, int n, uint8_t* dst)
+{
+    const int rows = c->rows, cols = c->cols;
+    if (!col_major) {
+        HIPC(c, hipMemcpy2DAsync(dst, cols, img, ld, cols, (size_t)rows * n, hipMemcpyHostToDevice, c->stream));
+        return VO_OK;
+    }
+    const size_t need = (size_t)ld * cols * n;
+    if (need > c->cm_cap) {
+        HIPC(c, hipStreamSynchronize(c->stream));
+        hipFree(c->d_cm);
+        c->d_cm = nullptr;
+        c->cm_cap = 0;
+        HIPC(c, hipMalloc((void**)&c->d_cm, need));
+        c->cm_cap = need;
+    }
+    HIPC(c, hipMemcpyAsync(c->d_cm, img, need, hipMemcpyHostToDevice, c->stream));
+    VO_LAUNCH(k_cm_to_rm_u8, dim3((rows + 31) / 32, (cols + 31) / 32, n), dim3(256), 0, c->stream, c->d_cm, ld, rows, cols, dst);
+    return VO_OK;
+}
+
+int vo_sift_ex(vo_ctx* c, const uint8_t* img, int rows, int cols, int ld, int col_major, vo_keypoint* kps, uint8_t* desc,
+               int capacity, int* n_out)
+{
+    if (!c || !img || rows != c->rows || cols != c->cols || (col_major != 0 && col_major != 1) ||
+        ld < (col_major ? rows : cols))
+        return fail(c, VO_ERR_ARG, "vo_sift: bad arguments");
     BEGIN_CALL(c);
-    HIPC(c, hipMemcpy2DAsync(c->d_img, cols, img, ld, cols, rows, hipMemcpyHostToDevice, c->stream));
+    int rc_stage = stage_images(c, img, ld, col_major, 1, c->d_img);
+    if (rc_stage) return rc_stage;
     ImageSrc src{c->d_img, c->d_img, (size_t)rows * cols, cols, 0};
     sift_enqueue(c->py, c->sb, src, 1, c->sp, c->stream, c->d_py);
     c->last_set = 0;                                   // vo_fetch_* now read this result (set 0)
@@ -438,14 +493,16 @@ int vo_sift(vo_ctx* c, const uint8_t* img, int rows, int cols, int ld, vo_keypoi
     return VO_OK;
 }
 
-int vo_match(vo_ctx* c, const uint8_t* F1, int n1, const uint8_t* F2, int n2, uint32_t* pairs, int capacity, int* n_pairs)
+int vo_sift(vo_ctx* c, const uint8_t* img, int rows, int cols, int ld, vo_keypoint* kps, uint8_t* desc, int capacity,
+            int* n_out)
 {
-    if (!c || n1 < 0 || n2 < 0 || (n1 && !F1) || (n2 && !F2)) return fail(c, VO_ERR_ARG, "vo_match: bad arguments");
-    if (n1 > c->sb.kp_cap || n2 > c->sb.kp_cap) return fail(c, VO_ERR_CAPACITY, "vo_match: more rows than max_keypoints");
-    BEGIN_CALL(c);
+    return vo_sift_ex(c, img, rows, cols, ld, 0, kps, desc, capacity, n_out);
+}
+
+// matchFeatures on the two staged descriptor sets d_fd[0] (n1 rows) / d_fd[1] (n2 rows)
+static int match_staged(vo_ctx* c, int n1, int n2, uint32_t* pairs, int capacity, int* n_pairs, const char* who)
+{
     int nn[2] = {n1, n2};
-    if (n1) HIPC(c, hipMemcpyAsync(c->d_fd[0], F1, (size_t)n1 * VO_DESC_LEN, hipMemcpyHostToDevice, c->stream));
-    if (n2) HIPC(c, hipMemcpyAsync(c->d_fd[1], F2, (size_t)n2 * VO_DESC_LEN, hipMemcpyHostToDevice, c->stream));
     HIPC(c, hipMemcpyAsync(c->d_fn, nn, sizeof(nn), hipMemcpyHostToDevice, c->stream));
     desc_meta_launch(c->d_fd[0], c->d_fm[0], n1, c->stream);
     desc_meta_launch(c->d_fd[1], c->d_fm[1], n2, c->stream);
@@ -462,8 +519,46 @@ int vo_match(vo_ctx* c, const uint8_t* F1, int n1, const uint8_t* F2, int n2, ui
         HIPC(c, hipMemcpy(jj.data(), c->d_mj, sizeof(int) * m, hipMemcpyDeviceToHost));
         for (int k = 0; k < m; ++k) { pairs[2 * k] = (uint32_t)ii[k] + 1; pairs[2 * k + 1] = (uint32_t)jj[k] + 1; }
     }
-    if (P > capacity) return fail(c, VO_ERR_CAPACITY, "vo_match: %d pairs exceed capacity %d", P, capacity);
+    if (P > capacity) return fail(c, VO_ERR_CAPACITY, "%s: %d pairs exceed capacity %d", who, P, capacity);
     return VO_OK;
+}
+
+int vo_match(vo_ctx* c, const uint8_t* F1, int n1, const uint8_t* F2, int n2, uint32_t* pairs, int capacity, int* n_pairs)
+{
+    if (!c || n1 < 0 || n2 < 0 || (n1 && !F1) || (n2 && !F2)) return fail(c, VO_ERR_ARG, "vo_match: bad arguments");
+    if (n1 > c->sb.kp_cap || n2 > c->sb.kp_cap) return fail(c, VO_ERR_CAPACITY, "vo_match: more rows than max_keypoints");
+    BEGIN_CALL(c);
+    if (n1) HIPC(c, hipMemcpyAsync(c->d_fd[0], F1, (size_t)n1 * VO_DESC_LEN, hipMemcpyHostToDevice, c->stream));
+    if (n2) HIPC(c, hipMemcpyAsync(c->d_fd[1], F2, (size_t)n2 * VO_DESC_LEN, hipMemcpyHostToDevice, c->stream));
+    return match_staged(c, n1, n2, pairs, capacity, n_pairs, "vo_match");
+}
+
+int vo_match_f32(vo_ctx* c, const float* F1, int n1, int ld1, const float* F2, int n2, int ld2, int col_major,
+                 uint32_t* pairs, int capacity, int* n_pairs)
+{
+    if (!c || n1 < 0 || n2 < 0 || (n1 && !F1) || (n2 && !F2) || (col_major != 0 && col_major != 1))
+        return fail(c, VO_ERR_ARG, "vo_match_f32: bad arguments");
+    if ((n1 && ld1 < (col_major ? n1 : VO_DESC_LEN)) || (n2 && ld2 < (col_major ? n2 : VO_DESC_LEN)))
+        return fail(c, VO_ERR_ARG, "vo_match_f32: leading dimension too small");
+    if (n1 > c->sb.kp_cap || n2 > c->sb.kp_cap) return fail(c, VO_ERR_CAPACITY, "vo_match_f32: more rows than max_keypoints");
+    BEGIN_CALL(c);
+    HIPC(c, hipMemsetAsync(c->d_bad, 0, sizeof(int), c->stream));
+    const float* src[2] = {F1, F2};
+    const int n[2] = {n1, n2}, ld[2] = {ld1, ld2};
+    for (int s = 0; s < 2; ++s) {
+        if (!n[s]) continue;
+        // the matrix as it lies in host memory (MATLAB: n x 128 column-major, ld = n), one copy
+        const size_t elems = col_major ? (size_t)ld[s] * (VO_DESC_LEN - 1) + n[s] : (size_t)ld[s] * (n[s] - 1) + VO_DESC_LEN;
+        if (elems > (size_t)c->sb.kp_cap * VO_DESC_LEN) return fail(c, VO_ERR_CAPACITY, "vo_match_f32: matrix exceeds staging");
+        HIPC(c, hipMemcpyAsync(c->d_ff[s], src[s], sizeof(float) * elems, hipMemcpyHostToDevice, c->stream));
+        pack_f32_desc_launch(c->d_ff[s], n[s], ld[s], col_major, c->d_fd[s], c->d_bad, c->stream);
+    }
+    int rc = match_staged(c, n1, n2, pairs, capacity, n_pairs, "vo_match_f32");
+    if (rc && rc != VO_ERR_CAPACITY) return rc;
+    int bad = 0;
+    HIPC(c, hipMemcpy(&bad, c->d_bad, sizeof(int), hipMemcpyDeviceToHost));
+    if (bad) return fail(c, VO_ERR_ARG, "vo_match_f32: descriptor values must be integers in [0, 255] (SIFT)");
+    return rc;
 }
 
 // SIFT + stereo match on B frames already in device memory.
@@ -796,19 +891,25 @@ int vo_step_batch_dev(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B, 
     return rc;
 }
 
-int vo_step_batch(vo_ctx* c, const uint8_t* lefts, const uint8_t* rights, int ld, int B, vo_step_out* outs)
+int vo_step_batch_ex(vo_ctx* c, const uint8_t* lefts, const uint8_t* rights, int ld, int col_major, int B, vo_step_out* outs)
 {
-    if (!c || !lefts || !rights || !outs || B < 1 || B > c->max_batch || ld < c->cols)
+    if (!c || !lefts || !rights || !outs || B < 1 || B > c->max_batch || (col_major != 0 && col_major != 1) ||
+        ld < (col_major ? c->rows : c->cols))
         return fail(c, VO_ERR_ARG, "vo_step_batch: bad arguments");
     BEGIN_CALL(c);
     const size_t fs = (size_t)c->rows * c->cols;
     uint8_t* dl = c->d_img;
     uint8_t* dr = c->d_img + fs * B;
-    HIPC(c, hipMemcpy2DAsync(dl, c->cols, lefts, ld, c->cols, (size_t)c->rows * B, hipMemcpyHostToDevice, c->stream));
-    HIPC(c, hipMemcpy2DAsync(dr, c->cols, rights, ld, c->cols, (size_t)c->rows * B, hipMemcpyHostToDevice, c->stream));
-    int rc = run_batch(c, dl, dr, B, outs);
+    int rc = stage_images(c, lefts, ld, col_major, B, dl);
+    if (!rc) rc = stage_images(c, rights, ld, col_major, B, dr);
+    if (!rc) rc = run_batch(c, dl, dr, B, outs);
     g_prof = nullptr;
     return rc;
+}
+
+int vo_step_batch(vo_ctx* c, const uint8_t* lefts, const uint8_t* rights, int ld, int B, vo_step_out* outs)
+{
+    return vo_step_batch_ex(c, lefts, rights, ld, 0, B, outs);
 }
 
 int vo_step(vo_ctx* c, const uint8_t* left, const uint8_t* right, int ld, vo_step_out* out)

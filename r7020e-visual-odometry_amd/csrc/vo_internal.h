@@ -192,5 +192,6 @@ void match_free(MatchBuffers& b);
 void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, const vo_match_params& p,
                   hipStream_t s);
 void desc_meta_launch(const uint8_t* desc, DescMeta* meta, int n, hipStream_t s);
+void pack_f32_desc_launch(const float* F, int n, int ld, int col_major, uint8_t* out, int* bad, hipStream_t s);
 
 }  // namespace vo

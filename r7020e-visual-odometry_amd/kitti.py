@@ -4,8 +4,9 @@
 Mirrors what `VO.m` does around its per-frame loop:
   * sequence layout and loading   -- `VO.m:13-17` (times.txt, image_0/image_1 PNG datastores),
     `VO.m:23-38` (calib.txt: P0/P1 rows read with `readmatrix`, columns 2:13, row-major 3x4);
-  * undistortImage (`VO.m:75-76`) is the identity: `cameraIntrinsics` is built with zero
-    distortion (`VO.m:50-51`), so frames go to libvo unchanged (`undistort_identity` states it);
+  * undistortImage (`VO.m:75-76`): restated (`undistort`), and with the zero-distortion
+    `cameraIntrinsics` of `VO.m:50-51` it is the identity on u8 images (`undistort_identity`
+    checks the sampling map), so frames go to libvo unchanged;
   * trajectory                    -- `VO.m:130-134` (`pose = pose * rel_pose`, `all_poses`),
     written in the KITTI 3x4 row-major pose format;
   * accuracy                      -- `PlotOnMap.m:1-26`: the reference's lagged xz error
@@ -131,11 +132,54 @@ def load_landmarks(path: str | os.PathLike) -> np.ndarray:
 # ---------------------------------------------------------------------------------------
 # sequence loading
 # ---------------------------------------------------------------------------------------
-def undistort_identity() -> bool:
-    """`VO.m:75-76` undistortImage with the zero-distortion intrinsics of `VO.m:50-51` is the
-    identity map (bilinear at integer sample positions, OutputView 'same'); frames are
-    passed through unchanged."""
-    return True
+def undistort_map(K: np.ndarray, dist, rows: int, cols: int):
+    """undistortImage's sampling map (`VO.m:75-76`, OutputView 'same'): output pixel (u, v)
+    samples the distorted image at K * distort(K^-1 [u, v, 1]) with the Brown-Conrady model
+    (radial k1, k2[, k3], tangential p1, p2; `cameraIntrinsics` RadialDistortion /
+    TangentialDistortion).  -> (us, vs) float64 [rows, cols] (0-based pixel coordinates)."""
+    K = np.asarray(K, np.float64)
+    k = list(dist) + [0.0] * (5 - len(dist))
+    k1, k2, p1, p2, k3 = k[0], k[1], k[2], k[3], k[4]
+    v, u = np.mgrid[0:rows, 0:cols].astype(np.float64)
+    fx, fy, s, cx, cy = K[0, 0], K[1, 1], K[0, 1], K[0, 2], K[1, 2]
+    y = (v - cy) / fy
+    x = (u - cx - s * y) / fx
+    r2 = x * x + y * y
+    rad = 1.0 + k1 * r2 + k2 * r2 * r2 + k3 * r2 * r2 * r2
+    xd = x * rad + 2.0 * p1 * x * y + p2 * (r2 + 2.0 * x * x)
+    yd = y * rad + p1 * (r2 + 2.0 * y * y) + 2.0 * p2 * x * y
+    return fx * xd + s * yd + cx, fy * yd + cy
+
+
+def undistort(img: np.ndarray, K: np.ndarray, dist=(0.0, 0.0, 0.0, 0.0)) -> np.ndarray:
+    """undistortImage(I, intrinsics) for a u8 image: bilinear interpolation at the
+    undistort_map positions, 0 outside the image, rounded back to u8 (MATLAB keeps the
+    input class)."""
+    img = np.asarray(img)
+    rows, cols = img.shape
+    us, vs = undistort_map(K, dist, rows, cols)
+    x0, y0 = np.floor(us), np.floor(vs)
+    fx, fy = us - x0, vs - y0
+    x0, y0 = x0.astype(np.int64), y0.astype(np.int64)
+    f = img.astype(np.float64)
+
+    def at(yy, xx):
+        ok = (yy >= 0) & (yy < rows) & (xx >= 0) & (xx < cols)
+        return np.where(ok, f[np.clip(yy, 0, rows - 1), np.clip(xx, 0, cols - 1)], 0.0)
+    out = (at(y0, x0) * (1 - fx) * (1 - fy) + at(y0, x0 + 1) * fx * (1 - fy)
+           + at(y0 + 1, x0) * (1 - fx) * fy + at(y0 + 1, x0 + 1) * fx * fy)
+    return np.clip(np.rint(out), 0, 255).astype(np.uint8)
+
+
+def undistort_identity(K: np.ndarray, dist=(0.0, 0.0, 0.0, 0.0), rows: int = 376, cols: int = 1241) -> bool:
+    """True when undistortImage cannot change any u8 image: every sample position of
+    undistort_map is within 1e-6 px of its own pixel, so the bilinear weights of the
+    neighbours are < 1e-6 and the rounded result is the input byte.  `VO.m:50-51` builds
+    cameraIntrinsics with zero distortion, which makes `VO.m:75-76` the identity: libvo takes
+    the frames unchanged, and KittiSequence checks this for its calibration."""
+    us, vs = undistort_map(K, dist, rows, cols)
+    v, u = np.mgrid[0:rows, 0:cols]
+    return bool(np.abs(us - u).max() < 1e-6 and np.abs(vs - v).max() < 1e-6)
 
 
 def _read_png(path: Path) -> np.ndarray:
@@ -164,11 +208,14 @@ class KittiSequence:
             raise FileNotFoundError(f"{d}: image_0/image_1 PNG lists missing or of different length")
         cal = read_calib(d / "calib.txt")
         self.P1, self.P2 = cal["P0"], cal["P1"]          # VO.m's p1 / p2 (left, right)
+        first = _read_png(self.left[0])
+        self.rows, self.cols = first.shape
+        # VO.m:50-51 (zero distortion) makes VO.m:75-76 undistortImage the identity
+        if not undistort_identity(self.P1[:, :3], rows=self.rows, cols=self.cols):
+            raise ValueError("undistortImage with these intrinsics is not the identity")
         self.times = read_times(d / "times.txt") if (d / "times.txt").exists() else None
         gt = self.root / "poses" / f"{self.seq}.txt"
         self.gt = read_poses(gt) if gt.exists() else None
-        first = _read_png(self.left[0])
-        self.rows, self.cols = first.shape
         self._pool = cf.ThreadPoolExecutor(max_workers=self.threads)
 
     def __len__(self) -> int:

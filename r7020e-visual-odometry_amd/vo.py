@@ -91,7 +91,8 @@ EXPORTS = [
     "vo_steps_pending", "vo_fetch_tracks", "vo_get_landmarks", "vo_reset",
     "vo_sift_match_batch_dev", "vo_fetch_keypoints", "vo_fetch_stereo_pairs", "vo_fetch_gaussian", "vo_stream", "vo_set_profiling",
     "vo_kernel_times", "vo_set_frame_index", "vo_set_concurrency",
-    "vo_set_landmark_frame", "vo_get_landmark_rows", "vo_landmarks_to_world",
+    "vo_set_landmark_frame", "vo_get_landmark_rows", "vo_landmarks_to_world", "vo_match_f32",
+    "vo_sift_ex", "vo_step_batch_ex",
 ]
 
 _lib = None
@@ -128,6 +129,11 @@ def load_library(path: str | os.PathLike | None = None):
     L.vo_last_error.restype = C.c_char_p
     L.vo_sift.argtypes = [vp, P(C.c_uint8), C.c_int, C.c_int, C.c_int, P(Keypoint), P(C.c_uint8), C.c_int, P(C.c_int)]
     L.vo_match.argtypes = [vp, P(C.c_uint8), C.c_int, P(C.c_uint8), C.c_int, P(C.c_uint32), C.c_int, P(C.c_int)]
+    L.vo_sift_ex.argtypes = [vp, P(C.c_uint8), C.c_int, C.c_int, C.c_int, C.c_int, P(Keypoint), P(C.c_uint8), C.c_int,
+                             P(C.c_int)]
+    L.vo_step_batch_ex.argtypes = [vp, P(C.c_uint8), P(C.c_uint8), C.c_int, C.c_int, C.c_int, P(StepOut)]
+    L.vo_match_f32.argtypes = [vp, P(C.c_float), C.c_int, C.c_int, P(C.c_float), C.c_int, C.c_int, C.c_int,
+                               P(C.c_uint32), C.c_int, P(C.c_int)]
     L.vo_track.argtypes = [vp, P(C.c_uint8), P(C.c_uint8), C.c_int, P(C.c_uint8), C.c_int, P(C.c_uint8), C.c_int,
                            P(C.c_uint32), C.c_int, P(C.c_int)]
     L.vo_triangulate.argtypes = [vp, P(C.c_float), P(C.c_float), C.c_int, P(C.c_double), P(C.c_double), P(C.c_double)]
@@ -228,13 +234,19 @@ class Context:
 
     # ---- detectSIFTFeatures + extractFeatures ----
     def sift(self, img: np.ndarray):
-        img = np.ascontiguousarray(img, np.uint8)
+        """A Fortran-ordered image (MATLAB's layout) goes to vo_sift_ex untransposed."""
+        img = np.asarray(img, np.uint8)
+        if img.strides[0] == 1 and img.ndim == 2 and img.shape[0] > 1:
+            col_major, ld = 1, img.strides[1]
+        else:
+            img = np.ascontiguousarray(img) if img.strides[1] != 1 else img
+            col_major, ld = 0, img.strides[0]
         cap = self.sift_params.max_keypoints
         kps = np.zeros(cap, KP_DTYPE)
         desc = np.zeros((cap, 128), np.uint8)
         n = C.c_int(0)
-        self._check(self.lib.vo_sift(self.h, _p(img, C.c_uint8), img.shape[0], img.shape[1], img.strides[0],
-                                     kps.ctypes.data_as(C.POINTER(Keypoint)), _p(desc, C.c_uint8), cap, C.byref(n)))
+        self._check(self.lib.vo_sift_ex(self.h, _p(img, C.c_uint8), img.shape[0], img.shape[1], ld, col_major,
+                                        kps.ctypes.data_as(C.POINTER(Keypoint)), _p(desc, C.c_uint8), cap, C.byref(n)))
         return kps[: n.value].copy(), desc[: n.value].copy()
 
     # ---- matchFeatures ----
@@ -246,6 +258,33 @@ class Context:
         n = C.c_int(0)
         self._check(self.lib.vo_match(self.h, _p(F1, C.c_uint8), F1.shape[0], _p(F2, C.c_uint8), F2.shape[0],
                                       _p(pairs, C.c_uint32), cap, C.byref(n)))
+        return pairs[: n.value].copy()
+
+    def match_f32(self, F1: np.ndarray, F2: np.ndarray) -> np.ndarray:
+        """matchFeatures on single-precision n x 128 matrices in their own storage order
+        (vo_match_f32): a Fortran-ordered array (MATLAB's layout) goes through without a
+        transpose, a C-ordered one (any row stride) likewise."""
+        def view(F):
+            F = np.asarray(F)
+            if F.dtype != np.float32 or F.ndim != 2 or F.shape[1] != 128:
+                raise VOError(VO_ERR_ARG, "match_f32: n x 128 float32 matrices")
+            if F.strides[0] == 4 and F.strides[1] % 4 == 0 and F.shape[0] > 0:       # column-major
+                return F, F.strides[1] // 4, 1
+            if F.strides[1] == 4 and F.strides[0] % 4 == 0:
+                return F, max(F.strides[0] // 4, 128), 0
+            F = np.ascontiguousarray(F)
+            return F, 128, 0
+        (A, la, ca), (B, lb, cb) = view(F1), view(F2)
+        if A.shape[0] and B.shape[0] and ca != cb:
+            B, lb, cb = (np.asfortranarray(B), B.shape[0], 1) if ca else (np.ascontiguousarray(B), 128, 0)
+        order = ca if A.shape[0] else cb
+        cap = max(A.shape[0], 1)
+        pairs = np.zeros((cap, 2), np.uint32)
+        n = C.c_int(0)
+        pa = A.ctypes.data_as(C.POINTER(C.c_float)) if A.shape[0] else None
+        pb = B.ctypes.data_as(C.POINTER(C.c_float)) if B.shape[0] else None
+        self._check(self.lib.vo_match_f32(self.h, pa, A.shape[0], la, pb, B.shape[0], lb, order,
+                                          _p(pairs, C.c_uint32), cap, C.byref(n)))
         return pairs[: n.value].copy()
 
     # ---- benchmark workload: SIFT + stereo match of B pairs resident on device ----
@@ -337,13 +376,21 @@ class Context:
         return out[: rows.value].copy()
 
     # ---- the VO.m loop body ----
-    def step_batch(self, lefts: np.ndarray, rights: np.ndarray) -> np.ndarray:
-        L = np.ascontiguousarray(lefts, np.uint8)
-        R = np.ascontiguousarray(rights, np.uint8)
+    def step_batch(self, lefts: np.ndarray, rights: np.ndarray, col_major: bool = False) -> np.ndarray:
+        """B frames [B, rows, cols]; with col_major the frames are handed over in MATLAB's
+        storage (each frame column-major: pixel (r, c) at c * rows + r)."""
+        L, R = np.asarray(lefts, np.uint8), np.asarray(rights, np.uint8)
         B = L.shape[0]
+        if col_major:
+            L = np.ascontiguousarray(np.swapaxes(L, 1, 2))       # [B, cols, rows] = B column-major frames
+            R = np.ascontiguousarray(np.swapaxes(R, 1, 2))
+            ld = L.shape[2]
+        else:
+            L, R = np.ascontiguousarray(L), np.ascontiguousarray(R)
+            ld = L.shape[2]
         outs = np.zeros(B, STEP_DTYPE)
-        self._check(self.lib.vo_step_batch(self.h, _p(L, C.c_uint8), _p(R, C.c_uint8), L.shape[2], B,
-                                           outs.ctypes.data_as(C.POINTER(StepOut))))
+        self._check(self.lib.vo_step_batch_ex(self.h, _p(L, C.c_uint8), _p(R, C.c_uint8), ld, 1 if col_major else 0, B,
+                                              outs.ctypes.data_as(C.POINTER(StepOut))))
         return outs
 
     def step_batch_dev(self, d_lefts: int, d_rights: int, B: int) -> np.ndarray:

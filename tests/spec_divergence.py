@@ -61,8 +61,9 @@ def pair_divergence(oracle, left, right):
     return {"left": a, "right": b, "n_match_spec": len(ps), "n_match_cv": len(pc), "match_jaccard": jac}
 
 
-def sequence_divergence(oracle, L, R, P1, P2):
-    """World poses of the VO.m loop under both implementations: max translation / rotation gap."""
+def sequence_divergence(oracle, L, R, P1, P2, gt=None):
+    """World poses of the VO.m loop under both implementations: max translation / rotation gap
+    (and, with the rendered ground truth gt [n, 4, 4], each one's max position error)."""
     os_, _ = oracle.run_sequence(L, R, P1, P2)
     oc, _ = oracle.run_sequence(L, R, P1, P2, cv=True)
     dt = np.linalg.norm(os_["pose"][:, :3, 3] - oc["pose"][:, :3, 3], axis=1)
@@ -70,4 +71,7 @@ def sequence_divergence(oracle, L, R, P1, P2):
     ang = np.degrees(np.arccos(np.clip((np.trace(Rrel, axis1=1, axis2=2) - 1) / 2, -1, 1)))
     step = np.linalg.norm(np.diff(os_["pose"][:, :3, 3], axis=0), axis=1)
     return {"frames": len(L), "max_translation_gap_m": float(dt.max()), "max_rotation_gap_deg": float(ang.max()),
-            "path_length_m": float(step.sum()), "status_spec": os_["status"].tolist(), "status_cv": oc["status"].tolist()}
+            "path_length_m": float(step.sum()), "status_spec": os_["status"].tolist(), "status_cv": oc["status"].tolist(),
+            **({} if gt is None else {
+                "max_error_spec_m": float(np.linalg.norm(os_["pose"][:, :3, 3] - (np.linalg.inv(gt[0]) @ gt)[:, :3, 3], axis=1).max()),
+                "max_error_cv_m": float(np.linalg.norm(oc["pose"][:, :3, 3] - (np.linalg.inv(gt[0]) @ gt)[:, :3, 3], axis=1).max())})}

@@ -89,3 +89,47 @@ def test_match_ragged_sizes_bit_exact(vo, oracle, n1, n2):
     ref = oracle.match(F1, F2)
     assert np.array_equal(got, ref)
     ctx.close()
+
+
+def test_match_f32_storage_orders_equal_u8_match(vo, oracle, syn):
+    """vo_match_f32 (single rows with ld and a storage-order flag, so a MEX gateway
+    passes MATLAB's column-major extractFeatures output zero-copy) == vo_match == oracle."""
+    L, R = syn.stereo_pair(syn.SEED_BASE + 77)
+    _, dl = oracle.sift(L)
+    _, dr = oracle.sift(R)
+    ref = oracle.match(dl, dr)
+    ctx = vo.Context(375, 1242, 1)
+    assert np.array_equal(ctx.match(dl, dr), ref)
+    fl, fr = dl.astype(np.float32), dr.astype(np.float32)
+    assert np.array_equal(ctx.match_f32(np.asfortranarray(fl), np.asfortranarray(fr)), ref)   # MATLAB layout
+    assert np.array_equal(ctx.match_f32(fl, fr), ref)                                         # row-major
+    pad = np.zeros((fl.shape[0], 160), np.float32)
+    pad[:, :128] = fl
+    assert np.array_equal(ctx.match_f32(pad[:, :128], fr), ref)                               # row stride 160
+    assert len(ctx.match_f32(np.zeros((0, 128), np.float32), fr)) == 0
+    bad = fl.copy()
+    bad[3, 7] = 0.5
+    with pytest.raises(vo.VOError):
+        ctx.match_f32(bad, fr)
+    ctx.close()
+
+
+def test_column_major_images_equal_row_major(vo, oracle, syn):
+    """vo_sift_ex / vo_step_batch_ex with col_major = 1 (MATLAB storage, device-side transpose)
+    give the row-major results bit for bit: SIFT of one image, and the loop body of 3 frames
+    (poses, landmark map)."""
+    L, R = syn.stereo_pair(syn.SEED_BASE + 88)
+    ctx = vo.Context(375, 1242, 3, calib=vo.calib_from(syn.KITTI00_P0, syn.KITTI00_P1))
+    k0, d0 = ctx.sift(L)
+    k1, d1 = ctx.sift(np.asfortranarray(L))
+    assert len(k0) > 500 and np.array_equal(k0, k1) and np.array_equal(d0, d1)
+    rk, rd = oracle.sift(L)
+    assert np.array_equal(k0, rk) and np.array_equal(d0, rd)
+    SL, SR, _ = syn.sequence(3)
+    a = ctx.step_batch(SL, SR)
+    la = ctx.get_landmarks()
+    ctx.reset()
+    b = ctx.step_batch(SL, SR, col_major=True)
+    lb = ctx.get_landmarks()
+    assert a.tobytes() == b.tobytes() and np.array_equal(la, lb)
+    ctx.close()

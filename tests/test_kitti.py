@@ -95,5 +95,21 @@ def test_sequence_loader_round_trip(kitti, syn, tmp_path):
     assert [g[0] for g in got] == [0, 2, 4]
     assert np.array_equal(np.concatenate([g[1] for g in got]), L)
     assert np.array_equal(np.concatenate([g[2] for g in got]), R)
-    assert kitti.undistort_identity()
+    assert kitti.undistort_identity(seq.P1[:, :3], rows=seq.rows, cols=seq.cols)
     seq.close()
+
+
+def test_undistort_zero_distortion_is_identity(kitti, syn):
+    """VO.m:50-51 builds cameraIntrinsics with zero distortion, so VO.m:75-76's undistortImage
+    returns every u8 frame unchanged (the frames go to libvo as they are); a non-zero
+    distortion does change them, so the check is not vacuous."""
+    L, _ = syn.stereo_pair(syn.SEED_BASE + 5)
+    K = syn.KITTI00_P0[:, :3]
+    assert kitti.undistort_identity(K, rows=375, cols=1242)
+    assert np.array_equal(kitti.undistort(L, K), L)
+    assert not kitti.undistort_identity(K, (-0.05, 0.0, 0.0, 0.0), rows=375, cols=1242)
+    out = kitti.undistort(L, K, (-0.05, 0.0, 0.0, 0.0))
+    assert (out != L).mean() > 0.2
+    # principal point: the map is the identity there even with radial distortion
+    us, vs = kitti.undistort_map(K, (-0.05, 0.01), 375, 1242)
+    assert abs(us[185, 607] - 607) < 0.2 and abs(vs[185, 607] - 185) < 0.3
