@@ -260,6 +260,11 @@ def main():
                                 "frac": per_launch / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
     else:
         roof.update({"achieved": None, "frac": None, "bytes_per_launch": None})
+    # every kernel the byte model prices: algorithmic GB/s in situ and isolated
+    roof["per_kernel_gbs"] = {
+        n: {"bytes_per_call": b, "in_situ": round(b / (kt[n][0] / args.profile_steps * 1e-3) / 1e9, 1),
+            "isolated": round(b / (kt_iso[n][0] / args.profile_steps * 1e-3) / 1e9, 1) if n in kt_iso else None}
+        for n, (b, _l) in model.items() if n in kt and kt[n][0] > 0}
     # whole-pyramid figure (SURVEY §8(d) per-frame model over the pyramid kernels' time)
     pyr_names = [n for n in kt if n.startswith(("k_blur", "k_down"))]
     pyr_ms = sum(kt[n][0] for n in pyr_names) / args.profile_steps

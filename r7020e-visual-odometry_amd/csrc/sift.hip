@@ -1083,20 +1083,22 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
 
 // Orientation assignment: one wave per accepted candidate (npk == -1).  Each
 // lane accumulates its samples' fixed-point weights (vo_desc_fx_quant, 2^-10)
-// into a private LDS row hp[lane][bin] (no contention; zeroed with 16-B
-// stores); the 36 bins are then summed over the 64 lanes in 64 bits (integer
-// sums: identical to the oracle's sequential total).  Samples are processed 4
-// per lane per iteration with every gradient load issued first.  Smoothing,
-// peak test and interpolation as the oracle.  (A lane's u32 partial of one bin
-// holds < 11k samples' weights: windows up to ~7e5 samples.)
+// into a private histogram hp[bin][lane]: lane l's words all lie in LDS bank l
+// (64 banks x 4 B), so the scattered per-sample adds of a wave never collide on
+// a bank (zeroed with 16-B stores); the 36 bins are then summed over the 64
+// lanes in 64 bits (integer sums: identical to the oracle's sequential total),
+// lane b reading bin b's partials in a rotated order so the 36 reading lanes
+// are on 36 distinct banks at every step.  Samples are processed 4 per lane per
+// iteration with every gradient load issued first.  Smoothing, peak test and
+// interpolation as the oracle.  (A lane's u32 partial of one bin holds < 11k
+// samples' weights: windows up to ~7e5 samples.)
 template <int HS>
 __global__ __launch_bounds__(64) void k_orient(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                                const int* __restrict__ n_cand, CandOut* __restrict__ cout,
                                                int cand_cap, int n_img)
 {
-    // HS: per-lane histogram stride.  Odd (37): lanes adding to the same bin hit distinct
-    // banks; 40 (= 8 mod 64 banks) put every 8th lane on one bank (k_orient ~2 % slower).
-    static_assert(HS >= VO_SIFT_ORI_BINS && (HS * 64) % 4 == 0, "per-lane rows hold the 36 bins");
+    // HS: bins per lane column (>= 36).  Layout hp[bin * 64 + lane].
+    static_assert(HS >= VO_SIFT_ORI_BINS && (HS * 64) % 4 == 0, "per-lane columns hold the 36 bins");
     __shared__ __attribute__((aligned(16))) uint32_t hp[HS * 64];
     __shared__ float tf[VO_SIFT_ORI_BINS];
     __shared__ float hs[VO_SIFT_ORI_BINS];
@@ -1154,13 +1156,13 @@ __global__ __launch_bounds__(64) void k_orient(const Pyramid* __restrict__ py, c
                 if (bin >= VO_SIFT_ORI_BINS) bin -= VO_SIFT_ORI_BINS;
                 if (bin < 0) bin += VO_SIFT_ORI_BINS;
                 const uint32_t qv = vo_desc_fx_quant((w * mag) * VO_DESC_FX_SCALE);
-                hp[lane * HS + bin] += okk[q] ? qv : 0u;          // private row; masked samples add 0
+                hp[bin * 64 + lane] += okk[q] ? qv : 0u;          // private column, bank = lane; masked samples add 0
             }
         }
         __syncthreads();
         if (lane < VO_SIFT_ORI_BINS) {
-            uint64_t acc = 0;                             // bin = lane: consecutive words per step
-            for (int q = 0; q < 64; ++q) acc += hp[q * HS + lane];
+            uint64_t acc = 0;                             // bin = lane; step q reads bank (q + lane) & 63
+            for (int q = 0; q < 64; ++q) acc += hp[lane * 64 + ((q + lane) & 63)];
             tf[lane] = vo_hist_fx_to_float(acc);
         }
         __syncthreads();
@@ -1266,14 +1268,20 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
 #define DHIST ((DW + 2) * (DW + 2) * DBS)
 // Histogram copies: lane l adds into copy (l & (DCOPIES-1)), so neighbouring samples
 // (same cell, often the same orientation bin) no longer serialise on one LDS address.
-// Copy stride 324 dwords = 4 mod 32 banks.  u32 fixed point (vo_desc_fx_quant) sums
-// are order-free, so the copies are folded after the loop without changing a bit.
+// Copy stride DCS = 324 dwords (= 4 mod 64 banks).  Measured (SQ_LDS_BANK_CONFLICT /
+// SQ_LDS_IDX_ACTIVE): 0.50 at 324; 0.62 at 336 (16 mod 64, disjoint bank windows for the 9
+// bins of a cell in the four copies), same k_desc time -- the adds scatter over cells and
+// orientation bins, and the LDS is ~46 % busy, so k_desc is bound by its per-sample VALU.
+// u32 fixed point (vo_desc_fx_quant) sums are order-free, so the copies are folded after
+// the loop without changing a bit.
+#define DCS 324
 template <int DCOPIES>
 __global__ __launch_bounds__(64, 5) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                              const KpInt* __restrict__ kpi, const int* __restrict__ n_kp,
                                              uint8_t* __restrict__ desc, DescMeta* __restrict__ meta, int kp_cap, int n_img)
 {
-    __shared__ uint32_t hfx[DCOPIES * DHIST];
+    static_assert(DCS >= DHIST, "copy stride holds a histogram");
+    __shared__ uint32_t hfx[DCOPIES * DCS];
     // per-row first column (16 bit: |j| <= RMAX) and exclusive sample prefix; a row's length is
     // rstart[r+1] - rstart[r].  < 8 KB of LDS in all -> 5 one-wave workgroups per SIMD
     __shared__ int16_t rlo[2 * VO_SIFT_DESCR_RMAX + 2];
@@ -1290,7 +1298,7 @@ __global__ __launch_bounds__(64, 5) void k_desc(const Pyramid* __restrict__ py, 
         const OctGeom& g = py->oct[q.o];
         const int rows = g.rows, cols = g.cols, P = g.pitch;
         const float* gim = arena + g.g_off[q.layer] + img * py->istride;
-        for (int b = lane; b < DCOPIES * DHIST; b += 64) hfx[b] = 0u;
+        for (int b = lane; b < DCOPIES * DCS; b += 64) hfx[b] = 0u;
         float ori = 360.0f - q.angle;
         if (fabsf(ori - 360.0f) < VO_FLT_EPSILON) ori = 0.0f;
         const int px = vo_round(q.xo), pyy = vo_round(q.yo);
@@ -1369,7 +1377,7 @@ __global__ __launch_bounds__(64, 5) void k_desc(const Pyramid* __restrict__ py, 
         }
         __syncthreads();
         const int nsamp = rstart[nrows];
-        uint32_t* hc = hfx + (lane & (DCOPIES - 1)) * DHIST;
+        uint32_t* hc = hfx + (lane & (DCOPIES - 1)) * DCS;
         int lo = 0;                                      // current row; s only grows, so advance
         constexpr int U = 4;                             // samples per lane per iteration: 16 loads in flight
         for (int s0 = lane; s0 < nsamp; s0 += 64 * U) {
@@ -1444,8 +1452,8 @@ __global__ __launch_bounds__(64, 5) void k_desc(const Pyramid* __restrict__ py, 
             uint32_t v = 0;
 #pragma unroll
             for (int cp = 0; cp < DCOPIES; ++cp) {
-                v += hfx[cp * DHIST + base + ob];
-                if (ob == 0) v += hfx[cp * DHIST + base + DN];
+                v += hfx[cp * DCS + base + ob];
+                if (ob == 0) v += hfx[cp * DCS + base + DN];
             }
             dv[h] = vo_desc_fx_to_float(v);
         }
@@ -1654,7 +1662,7 @@ void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const v
     VO_LAUNCH(k_seg_emit, gs, dim3(256), 0, s, d_py, b.mask, (const uint32_t*)b.woff, b.cand, b.cand_cap);
     VO_LAUNCH(k_refine, dim3(512), dim3(256), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.cand_cap, n_img,
               p.contrast_threshold, p.edge_threshold, p.sigma);
-    VO_LAUNCH_NAMED("k_orient", (k_orient<37>), dim3(kFeatureGrid), dim3(64), 0, s, d_py, A, b.n_cand,
+    VO_LAUNCH_NAMED("k_orient", (k_orient<36>), dim3(kFeatureGrid), dim3(64), 0, s, d_py, A, b.n_cand,
                     b.cout, b.cand_cap, n_img);
     VO_LAUNCH(k_scan_cands, dim3(n_img), dim3(1024), 0, s, b.cout, b.n_cand, b.koff, b.n_kp, b.cand_cap);
     VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, b.n_cand, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,

@@ -60,5 +60,5 @@ def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3) -> dict:
             add("k_down", 8 * px, 1)                                      # 1 of 4 source px in, G0 out
         add("k_blur_fused", 8 * px * lv, lv)                              # G_{i-1} in, G_i out
     # extremum test reads the L+3 Gaussian levels of every octave once (DoG formed on chip)
-    add(f"k_ext_tile<{layers}>", sum(4 * (layers + 3) * r * c for r, c in dims) * n_img, 1)
+    add(f"k_ext_stream<{layers}>", sum(4 * (layers + 3) * r * c for r, c in dims) * n_img, 1)
     return out

@@ -32,9 +32,11 @@ def test_kitti_driver_matches_host_stepping(vo, syn, tmp_path):
 
 
 def test_sharded_blocks_chain_to_single_run(vo, syn, tmp_path):
-    """Frame sharding (block + one-frame halo, MSAC keyed by the global frame index):
-    the ranks' relative poses, chained on the host, equal the single-process world poses
-    bit for bit (ranks simulated one after another on the one GPU of this box)."""
+    """Frame sharding (block + one-frame halo, MSAC keyed by the global frame index) of a
+    KITTI-layout sequence: the ranks' relative poses, chained on the host, and their
+    camera-frame landmark rows moved to the world after the chain equal the single-process
+    world poses and landmark map bit for bit (ranks simulated one after another on the one
+    GPU of this box)."""
     import vo_amd  # noqa: F401
     from r7020e_visual_odometry_amd import kitti, sharding
     from test_kitti import write_kitti_layout
@@ -42,11 +44,15 @@ def test_sharded_blocks_chain_to_single_run(vo, syn, tmp_path):
     L, R, _gt = syn.sequence(n, step_m=0.5)
     write_kitti_layout(tmp_path, L, R)
     seq = kitti.KittiSequence(tmp_path, "00")
-    poses, outs, _lm = kitti.run(seq, batch=3)
+    poses, outs, lm = kitti.run(seq, batch=3)
     for world in (2, 3):
-        rel = np.concatenate([kitti.run_shard(seq, r, world, batch=3) for r in range(world)])
-        assert rel.shape == (n, 4, 4)
-        assert np.array_equal(sharding.chain(rel), poses), world
+        parts = [kitti.run_shard(seq, r, world, batch=3) for r in range(world)]
+        o = np.concatenate([p[0] for p in parts])
+        assert o["rel_pose"].shape == (n, 4, 4)
+        assert np.array_equal(sharding.chain(o["rel_pose"]), poses), world
+        p2, lm2 = kitti.assemble(sharding.steps_of(o), np.concatenate([p[1] for p in parts]),
+                                 np.concatenate([p[2] for p in parts]))
+        assert np.array_equal(p2, poses) and np.array_equal(lm2, lm), world
     seq.close()
 
 

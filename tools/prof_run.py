@@ -10,7 +10,7 @@ from r7020e_visual_odometry_amd import vo, synthetic as syn
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-L, R = syn.independent_pairs(B)
+L, R = syn.independent_pairs(B, px_per_cell=syn.BENCH_PX_PER_CELL)
 dl, dr = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
 torch.cuda.synchronize()
 ctx = vo.Context(375, 1242, B)
