@@ -78,7 +78,13 @@ def launch_ranks(n: int) -> int:
     s.close()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + sys.argv[1:]
-    return subprocess.call(cmd)
+    # stdout carries exactly the JSON line: collective-library chatter (gloo prints its
+    # connection log to stdout) goes to stderr
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    for line in p.stdout:
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+        sys.stdout.flush()
+    return p.wait()
 
 
 def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks):

@@ -253,6 +253,14 @@ int vo_set_landmark_frame(vo_ctx* ctx, int camera);
 int vo_get_landmark_rows(vo_ctx* ctx, float* X, uint8_t* keep, int capacity, int* rows);
 /* Host-only, stateless: out[i] = keep[i] ? single(pose * [X[i]; 1]) : 0 (row-major 4x4 pose). */
 int vo_landmarks_to_world(const double pose[16], const float* X, const uint8_t* keep, int n, double* out);
+/* The same for a whole gathered sequence: frame f's rows_per_frame[f] consecutive rows with
+ * poses[f] (n_frames x 16 row-major); sum(rows_per_frame) must equal n_rows. */
+int vo_landmarks_to_world_frames(const double* poses, const int32_t* rows_per_frame, int n_frames, const float* X,
+                                 const uint8_t* keep, long n_rows, double* out);
+/* Host-only: the VO.m:130 world-pose chain over gathered relative poses (n x 16 row-major),
+ * pose = pose * rel[f] for frames whose status is VO_OK (status NULL: every frame), the pose
+ * after frame f into out[f]; pose0 NULL = identity.  Same arithmetic as vo_step_collect. */
+int vo_chain_poses(const double* rel, const int32_t* status, int n, const double* pose0, double* out);
 /* Reset loop state (features, pose, landmarks). */
 int vo_reset(vo_ctx* ctx);
 /* Global index of the next frame (the MSAC Philox key of frame i is

@@ -345,7 +345,7 @@ __device__ inline int xcd_remap(int bid, int n)
     return xcd < rm ? xcd * (q + 1) + idx : rm * (q + 1) + (xcd - rm) * q + idx;
 }
 
-#define BS_P 4            // prefetch depth (rows)
+#define BS_P 4            // prefetch depth (rows); 6 for the octave-0 base measured the same
 // halo floats each side, rounded up to whole CPL-column vectors; staged row length
 __host__ __device__ constexpr int bs_rh(int r, int cpl) { return (r + cpl - 1) / cpl * cpl; }
 __host__ __device__ constexpr int bs_rw(int r, int cpl) { return 64 * cpl + 2 * bs_rh(r, cpl); }
@@ -489,17 +489,31 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
 #pragma unroll
                 for (int i = 0; i < CPL; ++i) w[CPL * q + i] = t[i];
             }
-            float h[CPL];
+            // Row pass on column pairs (x, x+1), x = RH + 2c even: packed v_pk_add / v_pk_fma
+            // (IEEE per element: the scalar acc = k0*s0; acc = fmaf(kj, s[-j] + s[+j], acc)).
+            // Tap j reads the pairs {w[x-j], w[x+1-j]} and {w[x+j], w[x+1+j]}: aligned pairs
+            // E[m] = {w[2m], w[2m+1]} for even j, shifted pairs O[m] = {w[2m+1], w[2m+2]}
+            // (formed once per row) for odd j -- half the row-pass VALU of the scalar form.
+            constexpr int NW = CPL * NQ;
+            vo_f2 E[NW / 2], O[NW / 2 - 1];
 #pragma unroll
-            for (int i = 0; i < CPL; ++i) {
-                float acc = k[0] * w[RH + i];
+            for (int m = 0; m < NW / 2; ++m) E[m] = vo_f2{w[2 * m], w[2 * m + 1]};
+#pragma unroll
+            for (int m = 0; m < NW / 2 - 1; ++m) O[m] = __builtin_shufflevector(E[m], E[m + 1], 1, 2);
+#pragma unroll
+            for (int c = 0; c < NP; ++c) {
+                constexpr int X0 = RH;                    // x = X0 + 2c
+                const int x = X0 + 2 * c;
+                vo_f2 acc = vo_f2{k[0], k[0]} * E[x / 2];
                 if (!(TAG & 8))                           // TAG & 8: probe variant without the row pass
 #pragma unroll
-                    for (int j = 1; j <= RAD; ++j) acc = fmaf(k[j], w[RH + i - j] + w[RH + i + j], acc);
-                h[i] = acc;
+                    for (int j = 1; j <= RAD; ++j) {
+                        const vo_f2 a = (j & 1) ? O[(x - j - 1) / 2] : E[(x - j) / 2];
+                        const vo_f2 b = (j & 1) ? O[(x + j - 1) / 2] : E[(x + j) / 2];
+                        acc = __builtin_elementwise_fma(vo_f2{k[j], k[j]}, a + b, acc);
+                    }
+                H[2 * RAD + u][c] = acc;
             }
-#pragma unroll
-            for (int c = 0; c < NP; ++c) H[2 * RAD + u][c] = vo_f2{h[2 * c], h[2 * c + 1]};
             if constexpr (decltype(store_c)::value) {
                 vec_t g;
 #pragma unroll
@@ -562,17 +576,14 @@ __global__ __launch_bounds__(64, (RAD <= 6 || CPL == 2) ? 3 : 2) void k_blur_str
         blur_stream_body<RAD, false, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, TH, rb, u8);
 }
 
-// next octave base.  grid over outputs
-__global__ void k_down(const float* __restrict__ src, size_t splane, int spitch, float* __restrict__ dst, size_t dplane,
-                       int dpitch, int R, int C, int n_img)
+// next octave base: G0 of octave o = G_L of octave o-1 decimated by 2.  Grid (column blocks of
+// 256, rows, images): no index divisions (the grid-stride form spent ~57 VALU per element on
+// 64-bit div/mod).
+__global__ __launch_bounds__(256) void k_down(const float* __restrict__ src, size_t splane, int spitch,
+                                              float* __restrict__ dst, size_t dplane, int dpitch, int C)
 {
-    size_t n = (size_t)n_img * R * C;
-    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n; t += (size_t)gridDim.x * blockDim.x) {
-        int img = (int)(t / ((size_t)R * C));
-        int rem = (int)(t - (size_t)img * R * C);
-        int y = rem / C, x = rem - y * C;
-        dst[img * dplane + (size_t)y * dpitch + x] = src[img * splane + (size_t)(2 * y) * spitch + 2 * x];
-    }
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, img = blockIdx.z;
+    if (x < C) dst[img * dplane + (size_t)y * dpitch + x] = src[img * splane + (size_t)(2 * y) * spitch + 2 * x];
 }
 
 // ---------------------------------------------------------------------------
@@ -1514,7 +1525,10 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
         // latency-bound.  Level blurs of planes at most 1400 columns wide use 2 columns per
         // lane (128-column strips, half the ring registers): more waves and fewer idle lanes
         // at the narrow octaves, where the kernel is latency-bound rather than HBM-bound.
-        constexpr int kMaxTH = 128, kWaveTarget = 2048, kCpl2MaxC = 1400;
+#ifndef VO_CPL2_MAXC
+#define VO_CPL2_MAXC 1400
+#endif
+        constexpr int kMaxTH = 128, kWaveTarget = 2048, kCpl2MaxC = VO_CPL2_MAXC;
         const bool base = name[7] == 'b';
         const int cpl = (!base && C <= kCpl2MaxC) ? 2 : 4;
         const int n_strips = (C + 64 * cpl - 1) / (64 * cpl);
@@ -1620,12 +1634,8 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
             }
         } else {
             const OctGeom& pg = py.oct[o - 1];
-            size_t n = (size_t)n_img * R * C;
-            int blocks = (int)((n + 255) / 256);
-            if (blocks > 4096) blocks = 4096;
-            if (blocks < 1) blocks = 1;
-            VO_LAUNCH(k_down, dim3(blocks), dim3(256), 0, s, A + pg.g_off[L], py.istride, pg.pitch, A + g.g_off[0],
-                      py.istride, g.pitch, R, C, n_img);
+            VO_LAUNCH(k_down, dim3((C + 255) / 256, R, n_img), dim3(256), 0, s, A + pg.g_off[L], py.istride, pg.pitch,
+                      A + g.g_off[0], py.istride, g.pitch, C);
         }
         for (int i = 1; i < L + 3; ++i) {
             Kern K = make_kern(py, i);

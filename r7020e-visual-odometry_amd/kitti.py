@@ -371,10 +371,14 @@ def seq_calib(seq):
 def assemble(steps: dict, X: np.ndarray, keep: np.ndarray, to_world=None):
     """World poses (VO.m:130 chain, failed frames hold the pose) and the world landmark map
     (CreateLandmarksFromFeatures.m:17 per frame, after the chain) from gathered frame records
-    and camera-frame landmark rows."""
+    and camera-frame landmark rows.  Default: libvo's host functions (vo_chain_poses,
+    vo_landmarks_to_world_frames: one C call each); with `to_world` (the oracle's, in the
+    libvo-free tests) the Python chain of `sharding` and one call per frame."""
     from . import sharding
     if to_world is None:
-        from .vo import landmarks_to_world as to_world
+        from . import vo
+        poses = vo.chain_poses(steps["rel_pose"], steps["status"])
+        return poses, vo.landmarks_to_world_frames(poses, steps["n_landmarks"], X, keep)
     poses = sharding.chain(steps["rel_pose"], status=steps["status"])
     lm = sharding.world_landmarks(poses, steps["n_landmarks"], X, keep, to_world)
     return poses, lm

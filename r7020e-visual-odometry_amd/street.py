@@ -72,7 +72,7 @@ class StreetWorld:
 
     def __init__(self, centres: np.ndarray, seed: int = 0x5EED00, cell: float = 3.0,
                  street_half_width: float = 7.0, margin: float = 150.0, open_fringe: float = 0.3,
-                 facade_spacing: float = 0.46, ground_spacing: float = 0.36, device="cpu"):
+                 facade_spacing: float = 0.49, ground_spacing: float = 0.38, device="cpu"):
         import torch
         from scipy.spatial import cKDTree
         c = np.asarray(centres, np.float64)

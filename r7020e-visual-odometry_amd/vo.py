@@ -92,7 +92,7 @@ EXPORTS = [
     "vo_sift_match_batch_dev", "vo_fetch_keypoints", "vo_fetch_stereo_pairs", "vo_fetch_gaussian", "vo_stream", "vo_set_profiling",
     "vo_kernel_times", "vo_set_frame_index", "vo_set_concurrency",
     "vo_set_landmark_frame", "vo_get_landmark_rows", "vo_landmarks_to_world", "vo_match_f32",
-    "vo_sift_ex", "vo_step_batch_ex",
+    "vo_sift_ex", "vo_step_batch_ex", "vo_chain_poses", "vo_landmarks_to_world_frames",
 ]
 
 _lib = None
@@ -163,6 +163,9 @@ def load_library(path: str | os.PathLike | None = None):
     L.vo_set_landmark_frame.argtypes = [vp, C.c_int]
     L.vo_get_landmark_rows.argtypes = [vp, P(C.c_float), P(C.c_uint8), C.c_int, P(C.c_int)]
     L.vo_landmarks_to_world.argtypes = [P(C.c_double), P(C.c_float), P(C.c_uint8), C.c_int, P(C.c_double)]
+    L.vo_landmarks_to_world_frames.argtypes = [P(C.c_double), P(C.c_int32), C.c_int, P(C.c_float), P(C.c_uint8), C.c_long,
+                                               P(C.c_double)]
+    L.vo_chain_poses.argtypes = [P(C.c_double), P(C.c_int32), C.c_int, P(C.c_double), P(C.c_double)]
     L.vo_kernel_times.argtypes = [vp, P(C.c_char_p), P(C.c_double), P(C.c_int), C.c_int, P(C.c_int)]
     _lib = L
     return L
@@ -494,6 +497,33 @@ def landmarks_to_world(pose, X, keep) -> np.ndarray:
                                                _p(out, C.c_double))
     if rc != VO_OK:
         raise VOError(rc, "vo_landmarks_to_world: bad arguments")
+    return out
+
+
+def chain_poses(rel, status=None, pose0=None) -> np.ndarray:
+    """VO.m:130 world-pose chain (vo_chain_poses): frames with status != 0 hold the pose."""
+    rel = np.ascontiguousarray(rel, np.float64).reshape(-1, 16)
+    st = None if status is None else np.ascontiguousarray(status, np.int32).reshape(-1)
+    p0 = None if pose0 is None else np.ascontiguousarray(pose0, np.float64).reshape(16)
+    out = np.zeros((rel.shape[0], 16))
+    rc = load_library().vo_chain_poses(_p(rel, C.c_double), None if st is None else _p(st, C.c_int32), rel.shape[0],
+                                       None if p0 is None else _p(p0, C.c_double), _p(out, C.c_double))
+    if rc != VO_OK:
+        raise VOError(rc, "vo_chain_poses: bad arguments")
+    return out.reshape(-1, 4, 4)
+
+
+def landmarks_to_world_frames(poses, rows_per_frame, X, keep) -> np.ndarray:
+    """CreateLandmarksFromFeatures.m:17 for a whole gathered sequence (vo_landmarks_to_world_frames)."""
+    poses = np.ascontiguousarray(poses, np.float64).reshape(-1, 16)
+    n = np.ascontiguousarray(rows_per_frame, np.int32).reshape(-1)
+    X = np.ascontiguousarray(X, np.float32).reshape(-1, 3)
+    k = np.ascontiguousarray(keep, np.uint8).reshape(-1)
+    out = np.zeros((X.shape[0], 3))
+    rc = load_library().vo_landmarks_to_world_frames(_p(poses, C.c_double), _p(n, C.c_int32), poses.shape[0],
+                                                     _p(X, C.c_float), _p(k, C.c_uint8), X.shape[0], _p(out, C.c_double))
+    if rc != VO_OK:
+        raise VOError(rc, "vo_landmarks_to_world_frames: rows and per-frame counts disagree")
     return out
 
 

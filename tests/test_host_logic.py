@@ -35,3 +35,26 @@ def test_roofline_model_matches_survey():
     # octaves 4..8 (<= 9216 px per plane) are built by the single LDS-resident k_blur_small launch
     assert kb["k_blur_fused"][1] == 4 * 5 and kb["k_blur_base"][1] == 1 and kb["k_down"][1] == 3
     assert kb["k_blur_small"][1] == 1
+
+
+def test_libvo_host_chain_and_landmark_transform_equal_references(vo, oracle):
+    """vo_chain_poses / vo_landmarks_to_world_frames (host-only libvo entry points used after the
+    multi-GPU gathers; no GPU needed) == sharding.chain (libvo's collect arithmetic restated) and
+    the oracle's CreateLandmarksFromFeatures.m:17, bit for bit, with failed frames holding the pose."""
+    from r7020e_visual_odometry_amd import sharding
+    rng = np.random.default_rng(1)
+    rel = rng.normal(size=(60, 4, 4))
+    rel[:, 3] = [0, 0, 0, 1]
+    st = np.zeros(60, np.int64)
+    st[[0, 3, 17, 59]] = [0, -4, -3, -4]
+    poses = vo.chain_poses(rel, st)
+    assert np.array_equal(poses, sharding.chain(rel, status=st))
+    assert np.array_equal(poses[3], poses[2]) and np.array_equal(poses[17], poses[16])
+    n = rng.integers(0, 25, 60)
+    X = rng.normal(size=(n.sum(), 3)).astype(np.float32)
+    keep = rng.random(n.sum()) < 0.6
+    got = vo.landmarks_to_world_frames(poses, n, X, keep)
+    assert np.array_equal(got, sharding.world_landmarks(poses, n, X, keep, oracle.landmarks_to_world))
+    assert np.all(got[~keep] == 0)
+    with pytest.raises(vo.VOError):
+        vo.landmarks_to_world_frames(poses, n + 1, X, keep)

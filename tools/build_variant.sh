@@ -1,0 +1,19 @@
+#!/bin/bash
+# Build libvo with extra compile definitions into tools/variants/<name>/libvo.so (experiments;
+# bench.py / tests pick a variant up with VO_LIBPATH).   bash tools/build_variant.sh <name> -DX=Y ...
+# VO_SRC=<dir> builds from another copy of csrc (e.g. a git revision exported to /tmp).
+set -e
+NAME=$1; shift
+D=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$D/tools/variants/$NAME
+mkdir -p $OUT/obj
+cd ${VO_SRC:-$D/r7020e-visual-odometry_amd/csrc}
+FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I$D/include -I. $*"
+for f in sift match geom vo_api; do
+  X=""; [ $f = match ] && X="-mllvm -amdgpu-mfma-vgpr-form"
+  /opt/rocm/bin/hipcc $FL $X -c $f.hip -o $OUT/obj/$f.o &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libvo.so $OUT/obj/*.o
+rm -rf $OUT/obj
+echo built $OUT/libvo.so
