@@ -42,7 +42,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 I8_MFMA_PEAK_TOPS = 5000.0     # MI355X_MICROARCH.md "Matrix cores": I8 = 2x the dense BF16 ~2.5 PF per clock
 # per-launch HBM bytes of each kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes on this
 # workload (tools/pmc_passes.sh + tools/pmc_traffic.py; FETCH_SIZE doubled on gfx950)
-TRAFFIC_FILE = ROOT / "profiles" / "r01_pmc_traffic.json"
+# (the newest profiles/r<NN>_pmc_traffic.json)
+TRAFFIC_FILE = max(ROOT.glob("profiles/r*_pmc_traffic.json"), default=ROOT / "profiles" / "r01_pmc_traffic.json")
 
 
 def parse():
