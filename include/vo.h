@@ -27,6 +27,12 @@
  *   vo_step_collect        overlaps batch n's geometry and host pose chain
  *   vo_sift_match_batch    VO.m:79-87 for a batch of independent stereo pairs
  *                          (the benchmark workload, BASELINE.json configs[1])
+ *   vo_sift_ex /           the same calls taking MATLAB's column-major storage
+ *   vo_match_f32 /         (images, n x 128 single descriptors) without a host
+ *   vo_step_batch_ex       transpose or conversion (zero-copy MEX gateways)
+ *   vo_set_landmark_frame  sharded sequences: camera-frame landmark rows, moved
+ *   vo_landmarks_to_world* to the world after the gathered pose chain
+ *   vo_chain_poses         (CreateLandmarksFromFeatures.m:17, VO.m:130)
  *
  * Conventions
  *  - Return value: VO_OK (0) or a negative VO_ERR_* code.  vo_last_error()

@@ -346,6 +346,18 @@ __device__ inline int xcd_remap(int bid, int n)
 }
 
 #define BS_P 4            // prefetch depth (rows); 6 for the octave-0 base measured the same
+
+// Scale-space kernels raise their wave priority.  The feature stream's kernels (k_desc,
+// k_orient) are VALU-bound and run beside the scale space of the next batch; a SIMD arbitrates
+// VALU issue by priority, then age, so a freshly dispatched blur wave next to older descriptor
+// waves only got their leftover issue slots.
+#ifndef VO_SS_SETPRIO
+#define VO_SS_SETPRIO 2
+#endif
+__device__ __forceinline__ void vo_ss_prio()
+{
+    if constexpr (VO_SS_SETPRIO > 0) __builtin_amdgcn_s_setprio(VO_SS_SETPRIO);
+}
 // halo floats each side, rounded up to whole CPL-column vectors; staged row length
 __host__ __device__ constexpr int bs_rh(int r, int cpl) { return (r + cpl - 1) / cpl * cpl; }
 __host__ __device__ constexpr int bs_rw(int r, int cpl) { return 64 * cpl + 2 * bs_rh(r, cpl); }
@@ -556,6 +568,7 @@ __global__ __launch_bounds__(64, (RAD <= 6 || CPL == 2) ? 3 : 2) void k_blur_str
     const float* __restrict__ src, size_t splane, size_t dplane, int pitch, int R, int C, float* __restrict__ g_out, Kern K,
     int n_strips, int n_bands, int TH, ImageSrc isrc, int in_rows, int in_cols)
 {
+    vo_ss_prio();
     constexpr int RH = bs_rh(RAD, CPL), SW = 64 * CPL;
     __shared__ __attribute__((aligned(16))) float rb[bs_rw(RAD, CPL) + 64 * CPL];   // staged row + per-lane dummy halo slots
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -715,6 +728,7 @@ template <int L>
 __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                                    unsigned long long* __restrict__ mask, float thr, int n_img)
 {
+    vo_ss_prio();
     constexpr int NG = L + 3, ND = L + 2, W = 3;      // Gaussian levels, DoG levels, row window
     const int lane = threadIdx.x;
     const int u_all = xcd_remap(blockIdx.x, gridDim.x);
