@@ -1542,7 +1542,10 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
 #ifndef VO_CPL2_MAXC
 #define VO_CPL2_MAXC 1400
 #endif
-        constexpr int kMaxTH = 128, kWaveTarget = 2048, kCpl2MaxC = VO_CPL2_MAXC;
+#ifndef VO_BLUR_MAX_TH
+#define VO_BLUR_MAX_TH 128
+#endif
+        constexpr int kMaxTH = VO_BLUR_MAX_TH, kWaveTarget = 2048, kCpl2MaxC = VO_CPL2_MAXC;
         const bool base = name[7] == 'b';
         const int cpl = (!base && C <= kCpl2MaxC) ? 2 : 4;
         const int n_strips = (C + 64 * cpl - 1) / (64 * cpl);

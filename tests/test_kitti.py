@@ -113,3 +113,16 @@ def test_undistort_zero_distortion_is_identity(kitti, syn):
     # principal point: the map is the identity there even with radial distortion
     us, vs = kitti.undistort_map(K, (-0.05, 0.01), 375, 1242)
     assert abs(us[185, 607] - 607) < 0.2 and abs(vs[185, 607] - 185) < 0.3
+
+
+def test_reference_error_curve_fixture():
+    """The reference's published KITTI-00 accuracy (4500/error.png, VO.m on MATLAB over the real
+    images), digitised into a fixture by tests/golden/digitize_ref_error.py: 0..470.5 s (KITTI-00's
+    times.txt span), peak ~40.8 m near t = 460 s, final ~34.6 m."""
+    from pathlib import Path
+    d = np.loadtxt(Path(__file__).parent / "golden" / "kitti" / "ref_error_digitized.csv", delimiter=",")
+    t = np.loadtxt(Path(__file__).parent / "golden" / "kitti" / "times_00.txt")
+    assert len(d) > 500 and np.all(np.diff(d[:, 0]) > 0)
+    assert abs(d[-1, 0] - t[-1]) < 1.0
+    assert 40.0 < d[:, 1].max() < 41.5 and 450 < d[np.argmax(d[:, 1]), 0] < 470
+    assert 34.0 < d[-1, 1] < 35.3 and 13.5 < d[:, 1].mean() < 15.0
