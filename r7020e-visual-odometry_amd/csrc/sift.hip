@@ -361,7 +361,65 @@ __device__ __forceinline__ void vo_ss_prio()
 // halo floats each side, rounded up to whole CPL-column vectors; staged row length
 __host__ __device__ constexpr int bs_rh(int r, int cpl) { return (r + cpl - 1) / cpl * cpl; }
 __host__ __device__ constexpr int bs_rw(int r, int cpl) { return 64 * cpl + 2 * bs_rh(r, cpl); }
+// Row-window exchange of the streaming blur.  Each lane holds CPL consecutive columns of the
+// input row; the row pass needs r columns either side.  Halo-lane layout (bs_hl: 4-column lanes,
+// r <= VO_BLUR_DPP_MAXR): the wave covers 64*CPL input columns starting RH left of its output
+// strip, its outer RH/CPL lanes each side hold only halo columns and store nothing, and the
+// neighbours' columns arrive by whole-wave DPP shifts (wave_shr:1 / wave_shl:1, one VALU op
+// per column per level).  No halo loads, no halo upsampling, no LDS round trip: per row the
+// LDS exchange cost 2 ds_write_b128 (13 LDS cycles each, at half rate from one wave) + (1 +
+// 2 rh/4) ds_read_b128, which base_probe measured at ~180 of the octave-0 base kernel's ~430 us.
+#ifndef VO_BLUR_DPP_MAXR
+#define VO_BLUR_DPP_MAXR 5
+#endif
+#ifndef VO_BLUR_DPP_BASE_ONLY
+#define VO_BLUR_DPP_BASE_ONLY 0
+#endif
+__host__ __device__ constexpr bool bs_hl(int r, int cpl, int tag)
+{
+    return cpl == 4 && r <= VO_BLUR_DPP_MAXR && !(tag & 32) && (!VO_BLUR_DPP_BASE_ONLY || (tag & 1));
+}
+// output columns per strip
+__host__ __device__ constexpr int bs_sw(int r, int cpl, int tag) { return 64 * cpl - (bs_hl(r, cpl, tag) ? 2 * bs_rh(r, cpl) : 0); }
 
+enum : int { VO_DPP_WAVE_SHL1 = 0x130, VO_DPP_WAVE_SHR1 = 0x138 };
+template <int CTRL>
+__device__ __forceinline__ float vo_dpp(float src)
+{
+    // lane 0 (wave_shr) / lane 63 (wave_shl) has no source lane and keeps its own value
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(src), __float_as_int(src), CTRL, 0xF, 0xF, false));
+}
+
+// w[RH + j] = column (lane's first column + j) for j in [-RAD, CPL - 1 + RAD]: level s of the
+// window is the wave shifted by s lanes (only the components the row pass reads).  The first
+// and last RH/CPL lanes get shifted-in values they never use (they produce no output).
+template <int RAD, int CPL, typename vec_t>
+__device__ __forceinline__ void vo_dpp_window(const vec_t& vm, float* w)
+{
+    constexpr int RH = bs_rh(RAD, CPL), NL = RH / CPL;
+    float L[CPL], Rt[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) w[RH + k] = L[k] = Rt[k] = vm[k];
+#pragma unroll
+    for (int s = 1; s <= NL; ++s) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            if (k >= s * CPL - RAD) {
+                L[k] = vo_dpp<VO_DPP_WAVE_SHR1>(L[k]);
+                w[RH - s * CPL + k] = L[k];
+            }
+            if (CPL - 1 - k >= s * CPL - RAD) {
+                Rt[k] = vo_dpp<VO_DPP_WAVE_SHL1>(Rt[k]);
+                w[RH + s * CPL + k] = Rt[k];
+            }
+        }
+    }
+}
+
+
+#ifndef VO_UP_DOT4
+#define VO_UP_DOT4 1
+#endif
 // u8 source of the octave-0 base level (TAG & 4): the x2 upsample is formed
 // while staging each input row, from raw source words prefetched like floats.
 struct U8Src { const uint8_t* p; int ld, rows, cols; };
@@ -370,6 +428,20 @@ __device__ __forceinline__ vo_f4 up4_from_words(uint32_t a0, uint32_t a1, uint32
 {
     // 4 source bytes (columns g2-1 .. g2+2) of rows ya, yb -> outputs x .. x+3 (x = 2*g2), as up_sample
     const uint32_t ba = __builtin_amdgcn_alignbyte(a1, a0, sa), bb = __builtin_amdgcn_alignbyte(b1, b0, sb);
+#if VO_UP_DOT4
+    // up_sample's 0.75 ha + 0.25 hb, ha = 0.75 a + 0.25 b, is exact in fp32 for bytes (every
+    // partial is a multiple of 1/16 below 256), so it equals (9 A[xa] + 3 A[xb] + 3 B[xa] +
+    // B[xb]) / 16: one byte permute + one v_dot4_u32_u8 per output instead of ~10 VALU.
+    float r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t xa = 1 + (i >> 1), xb = (i & 1) ? xa + 1 : xa - 1;
+        const uint32_t sel = xa | xb << 8 | (4 + xa) << 16 | (4 + xb) << 24;   // bytes of {bb:ba}
+        const uint32_t q = __builtin_amdgcn_perm(bb, ba, sel);
+        r[i] = (float)__builtin_amdgcn_udot4(q, 0x01030309u, 0u, false) * 0.0625f;
+    }
+    return vo_f4{r[0], r[1], r[2], r[3]};
+#else
     float r[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -379,6 +451,7 @@ __device__ __forceinline__ vo_f4 up4_from_words(uint32_t a0, uint32_t a1, uint32
         r[i] = 0.75f * ha + 0.25f * hb;
     }
     return vo_f4{r[0], r[1], r[2], r[3]};
+#endif
 }
 
 template <int RAD, bool EDGE, int TAG, int CPL>
@@ -391,7 +464,8 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
     typedef float vec_t __attribute__((ext_vector_type(CPL)));
     constexpr bool UP = (TAG & 4) != 0;
     static_assert(!UP || CPL == 4, "the fused x2 upsample uses 4 columns per lane");
-    constexpr int SW = 64 * CPL;                           // strip width
+    constexpr bool XCH = bs_hl(RAD, CPL, TAG);             // halo-lane layout + DPP window exchange
+    constexpr int SW = 64 * CPL;                           // input columns per wave
     constexpr int P = BS_P;                                // prefetch depth = steps per loop block
     constexpr int RH = bs_rh(RAD, CPL);                    // halo rounded to whole vectors
     constexpr int NQ = 1 + 2 * RH / CPL;                   // vector reads per lane window
@@ -401,12 +475,12 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
     constexpr int E = F - 2 * RAD;                         // extra rows read above the band
     constexpr int RW = bs_rw(RAD, CPL);                    // staged row floats
     const int lane = threadIdx.x;
-    const int xl = x0 + CPL * lane;
+    const int xl = x0 - (XCH ? RH : 0) + CPL * lane;      // XCH: x0 is the first output column
     // halo lanes: [0, RH/CPL) left, [RH/CPL, 2*RH/CPL) right.  The others load lane 0's
     // segment (same cache line) and stage it into a private dummy LDS slot, so every
     // lane issues the same instructions.
     const bool hl = lane < RH / CPL, hr = !hl && lane < 2 * RH / CPL;
-    const int hx = hl ? x0 - RH + CPL * lane : hr ? x0 + SW + CPL * (lane - RH / CPL) : x0 - RH;
+    const int hx = XCH ? xl : hl ? x0 - RH + CPL * lane : hr ? x0 + SW + CPL * (lane - RH / CPL) : x0 - RH;
     const int hpos = hl ? CPL * lane : hr ? RH + SW + CPL * (lane - RH / CPL) : -1;
     float* const dummy = rb + RW + CPL * lane;
     int cm[CPL], ch[CPL];                                  // border strips: reflect-101 source columns
@@ -447,59 +521,79 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                 const uint8_t* rb_ = u8.p + (size_t)yb_ * u8.ld;                                  \
                 pw[SL][0] = *reinterpret_cast<const u2_t*>((uintptr_t)(ra_ + gm) & ~(uintptr_t)3); \
                 pw[SL][1] = *reinterpret_cast<const u2_t*>((uintptr_t)(rb_ + gm) & ~(uintptr_t)3); \
-                pw[SL][2] = *reinterpret_cast<const u2_t*>((uintptr_t)(ra_ + gh) & ~(uintptr_t)3); \
-                pw[SL][3] = *reinterpret_cast<const u2_t*>((uintptr_t)(rb_ + gh) & ~(uintptr_t)3); \
+                if constexpr (!XCH) {                                                             \
+                    pw[SL][2] = *reinterpret_cast<const u2_t*>((uintptr_t)(ra_ + gh) & ~(uintptr_t)3); \
+                    pw[SL][3] = *reinterpret_cast<const u2_t*>((uintptr_t)(rb_ + gh) & ~(uintptr_t)3); \
+                }                                                                                 \
             }                                                                                     \
         } else {                                                                                  \
             const float* rowp_ = sp + (size_t)yin_ * pitch;                                       \
             if constexpr (!EDGE) {                                                                \
                 pf[SL] = *reinterpret_cast<const vec_t*>(rowp_ + xl);                             \
-                if (!(TAG & 64)) ph[SL] = *reinterpret_cast<const vec_t*>(rowp_ + hx);            \
+                if (!(TAG & 64) && !XCH) ph[SL] = *reinterpret_cast<const vec_t*>(rowp_ + hx);   \
             } else {                                                                              \
                 pf[SL] = gather(rowp_, cm);                                                       \
-                ph[SL] = gather(rowp_, ch);                                                       \
+                if constexpr (!XCH) ph[SL] = gather(rowp_, ch);                                   \
             }                                                                                     \
         }                                                                                         \
     } while (0)
 
-    // P steps kk0 .. kk0+P-1: stage input row kk into LDS, prefetch row kk+P,
-    // horizontal pass into ring slot 2r+u, and (STORE) the vertical pass over ring
-    // slots u .. u+2r for output row y0 + kk - F; then the ring shifts down by P.
+    // row kk's own and halo vectors from prefetch slot SL (UP: the x2 upsample formed here)
+    auto fetch = [&](auto sl_c, int kk, vec_t& vm, vec_t& vh) {
+        constexpr int SL = decltype(sl_c)::value;
+        vm = pf[SL];
+        if constexpr (!XCH) vh = ph[SL];
+        if constexpr (UP) {
+            const int yin = vo_reflect101(y0 - RAD - E + kk, R);
+            if constexpr (!EDGE) {
+                const int ya = yin >> 1, yb = (yin & 1) ? min(ya + 1, u8.rows - 1) : max(ya - 1, 0);
+                const uintptr_t pb = reinterpret_cast<uintptr_t>(u8.p);   // byte misalignment incl. the image base
+                const uint32_t sa = (uint32_t)((pb + (size_t)ya * u8.ld + gm) & 3), sb = (uint32_t)((pb + (size_t)yb * u8.ld + gm) & 3);
+                vm = up4_from_words(pw[SL][0].x, pw[SL][0].y, sa, pw[SL][1].x, pw[SL][1].y, sb);
+                if constexpr (!XCH) {
+                    const uint32_t ha = (uint32_t)((pb + (size_t)ya * u8.ld + gh) & 3), hb = (uint32_t)((pb + (size_t)yb * u8.ld + gh) & 3);
+                    vh = up4_from_words(pw[SL][2].x, pw[SL][2].y, ha, pw[SL][3].x, pw[SL][3].y, hb);
+                }
+            } else {                                      // border strips: reflected columns, loads in place
+#pragma unroll
+                for (int i = 0; i < CPL; ++i) {
+                    vm[i] = up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, cm[i]);
+                    if constexpr (!XCH) vh[i] = up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, ch[i]);
+                }
+            }
+        }
+    };
+    // P steps kk0 .. kk0+P-1: exchange input row kk's window (DPP, or staged through LDS),
+    // prefetch row kk+P, horizontal pass into ring slot 2r+u, and (STORE) the vertical pass
+    // over ring slots u .. u+2r for output row y0 + kk - F; then the ring shifts down by P.
     auto block = [&](int kk0, auto store_c) {
         vo_static_for<P>([&](auto uc) {
             constexpr int u = decltype(uc)::value;
             const int kk = kk0 + u;
-            float* const row = rb;
-            vec_t vm = pf[u], vh = ph[u];
-            if constexpr (UP) {
-                const int yin = vo_reflect101(y0 - RAD - E + kk, R);
-                if constexpr (!EDGE) {
-                    const int ya = yin >> 1, yb = (yin & 1) ? min(ya + 1, u8.rows - 1) : max(ya - 1, 0);
-                    const uintptr_t pb = reinterpret_cast<uintptr_t>(u8.p);   // byte misalignment incl. the image base
-                    const uint32_t sa = (uint32_t)((pb + (size_t)ya * u8.ld + gm) & 3), sb = (uint32_t)((pb + (size_t)yb * u8.ld + gm) & 3);
-                    const uint32_t ha = (uint32_t)((pb + (size_t)ya * u8.ld + gh) & 3), hb = (uint32_t)((pb + (size_t)yb * u8.ld + gh) & 3);
-                    vm = up4_from_words(pw[u][0].x, pw[u][0].y, sa, pw[u][1].x, pw[u][1].y, sb);
-                    vh = up4_from_words(pw[u][2].x, pw[u][2].y, ha, pw[u][3].x, pw[u][3].y, hb);
-                } else {                                  // border strips: reflected columns, loads in place
-#pragma unroll
-                    for (int i = 0; i < CPL; ++i) {
-                        vm[i] = up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, cm[i]);
-                        vh[i] = up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, ch[i]);
-                    }
-                }
-            }
-            if (!(TAG & 32)) {                            // TAG & 32: probe variant without LDS staging
-                *reinterpret_cast<vec_t*>(row + RH + CPL * lane) = vm;
-                *reinterpret_cast<vec_t*>(hpos >= 0 ? row + hpos : dummy) = vh;
-            }
-            __syncthreads();                              // one-wave block: orders the LDS row only
-            VO_BS_LOAD(kk + P, u);
             float w[CPL * NQ];
+            if constexpr (XCH) {
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const vec_t t = (TAG & 32) ? (q & 1 ? vh : vm) : *reinterpret_cast<const vec_t*>(row + CPL * lane + CPL * q);
+                for (int i = 0; i < CPL * NQ; ++i) w[i] = 0.0f;
+                vec_t vm, vh;
+                fetch(uc, kk, vm, vh);
+                VO_BS_LOAD(kk + P, u);
+                vo_dpp_window<RAD, CPL>(vm, w);
+            } else {
+                float* const row = rb;
+                vec_t vm, vh;
+                fetch(uc, kk, vm, vh);
+                if (!(TAG & 32)) {                        // TAG & 32: probe variant without LDS staging
+                    *reinterpret_cast<vec_t*>(row + RH + CPL * lane) = vm;
+                    *reinterpret_cast<vec_t*>(hpos >= 0 ? row + hpos : dummy) = vh;
+                }
+                __syncthreads();                          // one-wave block: orders the LDS row only
+                VO_BS_LOAD(kk + P, u);
 #pragma unroll
-                for (int i = 0; i < CPL; ++i) w[CPL * q + i] = t[i];
+                for (int q = 0; q < NQ; ++q) {
+                    const vec_t t = (TAG & 32) ? (q & 1 ? vh : vm) : *reinterpret_cast<const vec_t*>(row + CPL * lane + CPL * q);
+#pragma unroll
+                    for (int i = 0; i < CPL; ++i) w[CPL * q + i] = t[i];
+                }
             }
             // Row pass on column pairs (x, x+1), x = RH + 2c even: packed v_pk_add / v_pk_fma
             // (IEEE per element: the scalar acc = k0*s0; acc = fmaf(kj, s[-j] + s[+j], acc)).
@@ -540,10 +634,13 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                 }
                 // columns >= C land in the row padding (pitch is a whole number of strips)
                 const size_t off = (size_t)(y0 + kk - F) * pitch + xl;
-                if (TAG & 2) *reinterpret_cast<vec_t*>(g_out + off) = g;            // cached store variant
-                else __builtin_nontemporal_store(g, reinterpret_cast<vec_t*>(g_out + off));
+                // XCH: the halo lanes store nothing; the last strip stops at the row pitch
+                if (!XCH || (lane >= RH / CPL && lane < 64 - RH / CPL && xl < pitch)) {
+                    if (TAG & 2) *reinterpret_cast<vec_t*>(g_out + off) = g;        // cached store variant
+                    else __builtin_nontemporal_store(g, reinterpret_cast<vec_t*>(g_out + off));
+                }
             }
-            __syncthreads();
+            if constexpr (!XCH) __syncthreads();
         });
 #pragma unroll
         for (int q = 0; q < 2 * RAD; ++q)
@@ -569,8 +666,10 @@ __global__ __launch_bounds__(64, (RAD <= 6 || CPL == 2) ? 3 : 2) void k_blur_str
     int n_strips, int n_bands, int TH, ImageSrc isrc, int in_rows, int in_cols)
 {
     vo_ss_prio();
-    constexpr int RH = bs_rh(RAD, CPL), SW = 64 * CPL;
-    __shared__ __attribute__((aligned(16))) float rb[bs_rw(RAD, CPL) + 64 * CPL];   // staged row + per-lane dummy halo slots
+    constexpr int RH = bs_rh(RAD, CPL), SW = bs_sw(RAD, CPL, TAG);   // output columns per strip
+    constexpr bool XCH = bs_hl(RAD, CPL, TAG);
+    // LDS exchange: staged row + per-lane dummy halo slots (unused with the DPP exchange)
+    __shared__ __attribute__((aligned(16))) float rb[XCH ? 4 : bs_rw(RAD, CPL) + 64 * CPL];
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int strip = bid % n_strips, tb = bid / n_strips;
     const int band = tb % n_bands, img = tb / n_bands;
@@ -583,7 +682,7 @@ __global__ __launch_bounds__(64, (RAD <= 6 || CPL == 2) ? 3 : 2) void k_blur_str
         u8.ld = isrc.ld;
         margin = 16;                                       // 8-B word loads stay inside the source row
     }
-    if (x0 - RH < 0 || x0 + SW + RH + margin > C)
+    if (x0 - RH < 0 || (XCH ? x0 - RH + 64 * CPL : x0 + SW + RH) + margin > C)
         blur_stream_body<RAD, true, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, TH, rb, u8);
     else
         blur_stream_body<RAD, false, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, TH, rb, u8);
@@ -1554,10 +1653,12 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
         TH = std::max(BS_P, TH / BS_P * BS_P);
         if (R >= TH) {
             const int n_bands = (R + TH - 1) / TH;
-            const int blocks = n_strips * n_bands * (int)grid.z;
-#define VO_BS_GO(T, CP)                                                                                               \
-    VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, T, CP>), dim3(blocks), dim3(64), 0, s, src, plane, dplane, pitch, R, C, g, \
-                    K, n_strips, n_bands, TH, isrc, in_rows, in_cols)
+#define VO_BS_GO(T, CP)                                                                                        \
+    do {                                                                                                       \
+        const int ns_ = (C + bs_sw(RAD, CP, T) - 1) / bs_sw(RAD, CP, T);                                       \
+        VO_LAUNCH_NAMED(name, (k_blur_stream<RAD, T, CP>), dim3(ns_ * n_bands * (int)grid.z), dim3(64), 0, s, src, plane, \
+                        dplane, pitch, R, C, g, K, ns_, n_bands, TH, isrc, in_rows, in_cols);                     \
+    } while (0)
             if (base && src == nullptr) VO_BS_GO(5, 4);      // "k_blur_base" from the u8 image (x2 upsample fused)
             else if (base) VO_BS_GO(1, 4);
             else if (cpl == 2) VO_BS_GO(0, 2);

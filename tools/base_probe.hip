@@ -1,0 +1,92 @@
+// base_probe.hip — where the octave-0 base kernel's time goes (instrumentation, not libvo).
+// k_blur_stream<5, TAG=5> builds G0 (x2 upsample fused, r = 5 blur) of 128 images of 375 x 1242
+// u8 into 750 x 2484 planes (pitch 2560), as bench's batch of 64 stereo frames does.  Variants:
+// TAG bits 8 (no row pass), 16 (no column pass), 32 (no LDS staging); and a write-only strip
+// reference (every wave stores its band rows, nothing else) = the floor of this store pattern.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I include -I r7020e-visual-odometry_amd/csrc tools/base_probe.hip -o tools/base_probe
+#include "../r7020e-visual-odometry_amd/csrc/sift.hip"
+#include <cstdio>
+
+using namespace vo;
+namespace vo {
+Profiler* g_prof = nullptr;
+void Profiler::begin(const char*, hipStream_t) {}
+void Profiler::end(hipStream_t) {}
+void Profiler::collect() {}
+void Profiler::reset_totals() {}
+Profiler::~Profiler() {}
+}
+
+template <int P>
+__global__ __launch_bounds__(64) void k_store_strip(float* __restrict__ b, int pitch, int R, size_t plane, int n_strips,
+                                                    int n_bands, int TH)
+{
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int strip = bid % n_strips, tb = bid / n_strips, band = tb % n_bands, img = tb / n_bands;
+    const int x0 = strip * 256, y0 = min(band * TH, R - TH);
+    const int xl = x0 + 4 * (int)threadIdx.x;
+    float* bp = b + img * plane;
+    const f4 v = {1.0f, 2.0f, 3.0f, (float)img};
+    for (int k = 0; k < TH; ++k)
+        __builtin_nontemporal_store(v, reinterpret_cast<f4*>(bp + (size_t)(y0 + k) * pitch + xl));
+}
+
+template <int TAG>
+static float run(const uint8_t* u8, float* dst, size_t plane, int pitch, int R, int C, int n_img, int TH, const Kern& K)
+{
+    constexpr int SW = bs_sw(5, 4, TAG);                  // output columns per strip (halo-lane layout: 240)
+    const int n_strips = (C + SW - 1) / SW, n_bands = (R + TH - 1) / TH;
+    const int blocks = n_strips * n_bands * n_img;
+    const size_t fs = (size_t)(R / 2) * (C / 2);
+    ImageSrc isrc{u8, u8 + fs * (n_img / 2), fs, C / 2, 0};
+    hipEvent_t a, b;
+    hipEventCreate(&a); hipEventCreate(&b);
+    for (int w = 0; w < 2; ++w)
+        hipLaunchKernelGGL((k_blur_stream<5, TAG, 4>), dim3(blocks), dim3(64), 0, 0, nullptr, 0, plane, pitch, R, C, dst, K,
+                           n_strips, n_bands, TH, isrc, R / 2, C / 2);
+    hipEventRecord(a);
+    for (int i = 0; i < 10; ++i)
+        hipLaunchKernelGGL((k_blur_stream<5, TAG, 4>), dim3(blocks), dim3(64), 0, 0, nullptr, 0, plane, pitch, R, C, dst, K,
+                           n_strips, n_bands, TH, isrc, R / 2, C / 2);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    return 100.0f * ms;
+}
+
+int main()
+{
+    const int R = 750, C = 2484, n = 128, pitch = 2560;
+    const size_t plane = (size_t)R * pitch;
+    float* dst;
+    uint8_t* u8;
+    hipMalloc(&dst, sizeof(float) * plane * n);
+    hipMalloc(&u8, (size_t)(R / 2) * (C / 2) * n);
+    hipMemset(u8, 77, (size_t)(R / 2) * (C / 2) * n);
+    Kern K{};
+    K.r = 5;
+    for (int j = 0; j <= 5; ++j) K.k[j] = 1.0f / 11;
+    const double gb = 4.0 * R * C * n / 1e9;
+    for (int TH : {32, 64, 128, 256}) {
+        const int n_strips = (C + 255) / 256, n_bands = (R + TH - 1) / TH;
+        hipEvent_t a, b;
+        hipEventCreate(&a); hipEventCreate(&b);
+        hipLaunchKernelGGL(k_store_strip<4>, dim3(n_strips * n_bands * n), dim3(64), 0, 0, dst, pitch, R, plane, n_strips, n_bands, TH);
+        hipEventRecord(a);
+        for (int i = 0; i < 10; ++i)
+            hipLaunchKernelGGL(k_store_strip<4>, dim3(n_strips * n_bands * n), dim3(64), 0, 0, dst, pitch, R, plane, n_strips, n_bands, TH);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        const float t0 = run<5>(u8, dst, plane, pitch, R, C, n, TH, K);
+        const float t8 = run<5 | 8>(u8, dst, plane, pitch, R, C, n, TH, K);
+        const float t24 = run<5 | 24>(u8, dst, plane, pitch, R, C, n, TH, K);
+        const float t56 = run<5 | 56>(u8, dst, plane, pitch, R, C, n, TH, K);
+        printf("TH %3d: store-only %6.1f us (%5.2f TB/s) | base %6.1f us (%5.2f TB/s) | no-row %6.1f | no row/col %6.1f | "
+               "no row/col/LDS %6.1f\n", TH, 100.0f * ms, gb / (100.0f * ms) * 1e3, t0, gb / t0 * 1e3, t8, t24, t56);
+    }
+    return 0;
+}
