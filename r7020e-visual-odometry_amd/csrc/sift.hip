@@ -63,10 +63,11 @@ void build_pyramid_geometry(Pyramid& py, int rows, int cols, int n_img, const vo
         if (ir < 0) ir = 0;
         if (ic < 0) ic = 0;
         // words of 64 absolute columns covering the interior [BORDER, cols - BORDER)
-        py.wrow[o] = ic > 0 ? (py.oct[o].cols - VO_SIFT_BORDER - 1) / 64 + 1 : 0;
+        // (an even count: the extremum test writes a strip's two words as a pair, see k_ext_stream)
+        py.wrow[o] = ic > 0 ? ((py.oct[o].cols - VO_SIFT_BORDER - 1) / 64 + 2) / 2 * 2 : 0;
         for (int l = 0; l < L; ++l) { py.wbase[b++] = w; w += ir * py.wrow[o]; }
         py.ebase[o] = t;
-        py.estrips[o] = ic > 0 ? (py.wrow[o] + 1) / 2 : 0;
+        py.estrips[o] = py.wrow[o] / 2;
         t += py.estrips[o] * ((ir + VO_EXT_BAND - 1) / VO_EXT_BAND);
     }
     py.wbase[b] = w;
@@ -799,28 +800,29 @@ __device__ __forceinline__ void decode_word(const Pyramid* __restrict__ py, int 
 
 // ---------------------------------------------------------------------------
 // 26-neighbour extremum test, streaming.  One wave per (image, octave, strip
-// of 128 columns, band of VO_EXT_BAND interior rows); lane l owns columns
-// xs+l and xs+64+l, so a ballot over the lanes is a whole 64-column mask word (no
-// bit interleaving on the scalar unit).  The wave walks the band's rows (+1 above
-// and below): per row it loads the L+3 Gaussian levels (two coalesced 4-B loads +
-// one halo column: xs-1 in lane 0, xs+128 in lane 63), forms D_l = G_{l+1} - G_l
-// (never stored), reduces each level to its
-// horizontal 3-max/3-min (neighbours by lane shuffle), and keeps the last 3
-// rows of those in a register window (rows unrolled by 3, static slots).
-// Row t-1 is then tested: val >= max of its 3x3x3 block (val included)
-// <=> val >= all 26 neighbours.  The two ballots per (row, layer) are the two
-// 64-column mask words of the strip.  Input rows are prefetched 3 rows ahead.
+// of 128 columns, band of VO_EXT_BAND interior rows); lane l owns the adjacent
+// columns xs+2l and xs+2l+1.  The wave walks the band's rows (+1 above and below):
+// per row it loads the L+3 Gaussian levels (one coalesced 8-B load + one halo
+// column: xs-1 in lane 0, xs+128 in lane 63), forms D_l = G_{l+1} - G_l (never
+// stored), reduces each level to its horizontal 3-max/3-min -- the outer neighbours
+// xs+2l-1 and xs+2l+2 arrive by one DPP wave shift each, lanes 0 / 63 keeping their
+// halo column -- and keeps the last 3 rows of those in a register window (rows
+// unrolled by 3, static slots).  Row t-1 is then tested: val >= max of its 3x3x3
+// block (val included) <=> val >= all 26 neighbours.  The two ballots per (row,
+// layer) are the strip's even- and odd-column words (bit l = column xs+2l+c);
+// k_seg_emit interleaves each pair back into column order.  Input rows are
+// prefetched 3 rows ahead.
 // ---------------------------------------------------------------------------
 
 // whole-wave lane shifts on the VALU (GFX9 DPP wave_shr:1 / wave_shl:1) instead of
 // LDS-routed ds_bpermute shuffles; the lane without a source keeps its own value
-__device__ __forceinline__ float vo_wave_shr1(float x)      // lane i <- lane i-1
+__device__ __forceinline__ float vo_wave_shr1_or(float old, float x)   // lane i <- lane i-1; lane 0 <- old
 {
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), 0x138, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(x), 0x138, 0xf, 0xf, false));
 }
-__device__ __forceinline__ float vo_wave_shl1(float x)      // lane i <- lane i+1
+__device__ __forceinline__ float vo_wave_shl1_or(float old, float x)   // lane i <- lane i+1; lane 63 <- old
 {
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), 0x130, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(x), 0x130, 0xf, 0xf, false));
 }
 
 template <int L>
@@ -845,7 +847,7 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
     const int ir = rows - 2 * VO_SIFT_BORDER;
     const int r0 = VO_SIFT_BORDER + band * VO_EXT_BAND;                 // first tested row
     const int nrow = min(VO_EXT_BAND, ir - band * VO_EXT_BAND);          // tested rows in this band
-    const int xs = strip * 128, xa = xs + lane, xb = xa + 64;
+    const int xs = strip * 128, xa = xs + 2 * lane, xb = xa + 1;
     // halo columns: lane 63 -> xs+128, the others xs-1 (used by lane 0; same cache line)
     const int hx = lane == 63 ? xs + 128 : max(xs - 1, 0);
     const float* base = arena + img * py->istride;
@@ -861,7 +863,7 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
     const bool in1 = xb >= VO_SIFT_BORDER && xb < cols - VO_SIFT_BORDER;
 
     typedef float f2_t __attribute__((ext_vector_type(2)));
-    f2_t pm[W][NG];                                  // prefetched columns {xa, xb}, per window slot
+    f2_t pm[W][NG];                                  // prefetched columns {xa, xa+1}, per window slot
     float ph[W][NG];                                 // prefetched halo column
     f2_t hmx[W][ND], hmn[W][ND];                     // horizontal 3-max / 3-min per row slot
     f2_t dc[W][L];                                   // D of layers 1..L per row slot (centres)
@@ -871,7 +873,7 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
         const int y_ = min(r0 - 1 + (T), rows - 1);                                                \
         const float* rp_ = base + (size_t)y_ * pitch;                                              \
         _Pragma("unroll") for (int lv = 0; lv < NG; ++lv) {                                        \
-            pm[SL][lv] = f2_t{rp_[goff[lv] + xa], rp_[goff[lv] + xb]};                             \
+            pm[SL][lv] = *reinterpret_cast<const f2_t*>(rp_ + goff[lv] + xa);                     \
             ph[SL][lv] = rp_[goff[lv] + hx];                                                       \
         }                                                                                          \
     } while (0)
@@ -889,16 +891,11 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
         VO_ET_LOAD(t + W, SL);                        // refill the slot with row t+3
 #pragma unroll
         for (int lv = 0; lv < ND; ++lv) {
-            // neighbours of xa: xa-1 (lane 0: halo xs-1), xa+1 (lane 63: xs+64 = lane 0's xb);
-            // of xb: xb-1 (lane 0: xs+63 = lane 63's xa), xb+1 (lane 63: halo xs+128)
-            float la = vo_wave_shr1(d[lv].x), ra = vo_wave_shl1(d[lv].x);
-            float lb = vo_wave_shr1(d[lv].y), rb = vo_wave_shl1(d[lv].y);
-            const float b0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d[lv].y), 0));
-            const float a63 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d[lv].x), 63));
-            if (lane == 0) { la = hd[lv]; lb = a63; }
-            if (lane == 63) { ra = b0; rb = hd[lv]; }
-            hmx[SL][lv] = f2_t{fmaxf(fmaxf(la, d[lv].x), ra), fmaxf(fmaxf(lb, d[lv].y), rb)};
-            hmn[SL][lv] = f2_t{fminf(fminf(la, d[lv].x), ra), fminf(fminf(lb, d[lv].y), rb)};
+            // outer neighbours: xa-1 = lane l-1's xb (lane 0: its halo xs-1), xb+1 = lane
+            // l+1's xa (lane 63: its halo xs+128) -- a lane without a source keeps `old` = hd
+            const float la = vo_wave_shr1_or(hd[lv], d[lv].y), rb = vo_wave_shl1_or(hd[lv], d[lv].x);
+            hmx[SL][lv] = f2_t{fmaxf(fmaxf(la, d[lv].x), d[lv].y), fmaxf(fmaxf(d[lv].x, d[lv].y), rb)};
+            hmn[SL][lv] = f2_t{fminf(fminf(la, d[lv].x), d[lv].y), fminf(fminf(d[lv].x, d[lv].y), rb)};
         }
 #pragma unroll
         for (int l = 0; l < L; ++l) dc[SL][l] = d[l + 1];
@@ -923,14 +920,12 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
                                             c ? mx3[layer + 1].y : mx3[layer + 1].x);
                     const float bmn = fminf(fminf(c ? mn3[layer - 1].y : mn3[layer - 1].x, c ? mn3[layer].y : mn3[layer].x),
                                             c ? mn3[layer + 1].y : mn3[layer + 1].x);
-                    // branch-free form of |val| > thr && (val > 0 ? val >= bmx : val <= bmn):
-                    // negation by the sign select is exact
-                    const float sg = val > 0 ? 1.0f : -1.0f, ref = val > 0 ? bmx : bmn;
-                    e[c] = (fabsf(val) > thr) & (sg * val >= sg * ref);
+                    // |val| > thr && (val > 0 ? val >= bmx : val <= bmn), as lane-mask compares
+                    e[c] = ((val > thr) & (val >= bmx)) | ((val < -thr) & (val <= bmn));
                 }
-                const uint64_t w0 = __ballot(e[0] && in0), w1 = __ballot(e[1] && in1);
-                const int k = 2 * strip + lane;
-                if (lane < 2 && k < wr && t - 2 < nrow)
+                const uint64_t w0 = __ballot(e[0] & in0), w1 = __ballot(e[1] & in1);
+                const int k = 2 * strip + lane;               // wr is even: both words exist
+                if (lane < 2 && t - 2 < nrow)
                     mrow[wb[layer - 1] + (size_t)(r - VO_SIFT_BORDER) * wr + k] = lane ? w1 : w0;
             }
         }
@@ -1025,6 +1020,18 @@ __device__ __forceinline__ uint32_t block_exscan_256(uint32_t v, uint32_t* sh)
     return before + x - v;
 }
 
+// bit i of x -> bit 2i
+__device__ __forceinline__ unsigned long long vo_spread32(uint32_t x)
+{
+    unsigned long long v = x;
+    v = (v | v << 16) & 0x0000FFFF0000FFFFull;
+    v = (v | v << 8) & 0x00FF00FF00FF00FFull;
+    v = (v | v << 4) & 0x0F0F0F0F0F0F0F0Full;
+    v = (v | v << 2) & 0x3333333333333333ull;
+    v = (v | v << 1) & 0x5555555555555555ull;
+    return v;
+}
+
 __global__ __launch_bounds__(256) void k_seg_emit(const Pyramid* __restrict__ py, const unsigned long long* __restrict__ mask,
                                                   const uint32_t* __restrict__ segoff, uint32_t* __restrict__ cand,
                                                   int cand_cap)
@@ -1040,6 +1047,14 @@ __global__ __launch_bounds__(256) void k_seg_emit(const Pyramid* __restrict__ py
     for (int q = 0; q < 4; ++q) {
         mw[q] = (w0 + q < nw) ? m[w0 + q] : 0ull;
         cnt += (uint32_t)__popcll(mw[q]);
+    }
+    // k_ext_stream writes a strip's words as (even columns, odd columns); w0 and every mask
+    // row start are even, so each (q, q+1) pair is one strip: interleave into column order
+#pragma unroll
+    for (int q = 0; q < 4; q += 2) {
+        const unsigned long long ev = mw[q], od = mw[q + 1];
+        mw[q] = vo_spread32((uint32_t)ev) | vo_spread32((uint32_t)od) << 1;
+        mw[q + 1] = vo_spread32((uint32_t)(ev >> 32)) | vo_spread32((uint32_t)(od >> 32)) << 1;
     }
     uint32_t idx = segoff[(size_t)img * py->n_seg + seg] + block_exscan_256(cnt, sh);
     if (!cnt) return;
