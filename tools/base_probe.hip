@@ -6,6 +6,7 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I include -I r7020e-visual-odometry_amd/csrc tools/base_probe.hip -o tools/base_probe
 #include "../r7020e-visual-odometry_amd/csrc/sift.hip"
 #include <cstdio>
+#include <hip/hip_ext.h>
 
 using namespace vo;
 namespace vo {
@@ -33,7 +34,8 @@ __global__ __launch_bounds__(64) void k_store_strip(float* __restrict__ b, int p
 }
 
 template <int TAG>
-static float run(const uint8_t* u8, float* dst, size_t plane, int pitch, int R, int C, int n_img, int TH, const Kern& K)
+static float run(const uint8_t* u8, float* dst, size_t plane, int pitch, int R, int C, int n_img, int TH, const Kern& K,
+                 hipStream_t st = 0)
 {
     constexpr int SW = bs_sw(5, 4, TAG);                  // output columns per strip (halo-lane layout: 240)
     const int n_strips = (C + SW - 1) / SW, n_bands = (R + TH - 1) / TH;
@@ -43,13 +45,13 @@ static float run(const uint8_t* u8, float* dst, size_t plane, int pitch, int R, 
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
     for (int w = 0; w < 2; ++w)
-        hipLaunchKernelGGL((k_blur_stream<5, TAG, 4>), dim3(blocks), dim3(64), 0, 0, nullptr, 0, plane, pitch, R, C, dst, K,
+        hipLaunchKernelGGL((k_blur_stream<5, TAG, 4>), dim3(blocks), dim3(64), 0, st, nullptr, 0, plane, pitch, R, C, dst, K,
                            n_strips, n_bands, TH, isrc, R / 2, C / 2);
-    hipEventRecord(a);
+    hipEventRecord(a, st);
     for (int i = 0; i < 10; ++i)
-        hipLaunchKernelGGL((k_blur_stream<5, TAG, 4>), dim3(blocks), dim3(64), 0, 0, nullptr, 0, plane, pitch, R, C, dst, K,
+        hipLaunchKernelGGL((k_blur_stream<5, TAG, 4>), dim3(blocks), dim3(64), 0, st, nullptr, 0, plane, pitch, R, C, dst, K,
                            n_strips, n_bands, TH, isrc, R / 2, C / 2);
-    hipEventRecord(b);
+    hipEventRecord(b, st);
     hipEventSynchronize(b);
     float ms;
     hipEventElapsedTime(&ms, a, b);
@@ -87,6 +89,17 @@ int main()
         const float t56 = run<5 | 56>(u8, dst, plane, pitch, R, C, n, TH, K);
         printf("TH %3d: store-only %6.1f us (%5.2f TB/s) | base %6.1f us (%5.2f TB/s) | no-row %6.1f | no row/col %6.1f | "
                "no row/col/LDS %6.1f\n", TH, 100.0f * ms, gb / (100.0f * ms) * 1e3, t0, gb / t0 * 1e3, t8, t24, t56);
+    }
+    // the same base kernel on CU-masked streams (bit i set when i % div == 0)
+    int n_cu = 0;
+    hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, 0);
+    for (int div : {1, 2, 4, 8}) {
+        uint32_t m[16] = {};
+        for (int i = 0; i < n_cu && i < 512; ++i)
+            if (i % div == 0) m[i / 32] |= 1u << (i % 32);
+        hipStream_t st;
+        hipExtStreamCreateWithCUMask(&st, (uint32_t)((n_cu + 31) / 32), m);
+        printf("CU mask 1/%d: base %6.1f us (TH 128)\n", div, run<5>(u8, dst, plane, pitch, R, C, n, 128, K, st));
     }
     return 0;
 }
