@@ -1,13 +1,6 @@
 // vo_api.hip — the C-ABI of libvo (include/vo.h): context, staging and the
 // orchestration of the per-frame pipeline on one HIP stream.
 #include "vo_internal.h"
-#include <hip/hip_ext.h>
-#ifndef VO_FEAT_CU_Q
-#define VO_FEAT_CU_Q 0
-#endif
-#ifndef VO_SS_CU_EXCL
-#define VO_SS_CU_EXCL 0
-#endif
 #include "vo_geom.h"
 #include <cstdio>
 #include <cstring>
@@ -248,28 +241,9 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
         // every stream at the default priority: the forked SIFT streams must not rank below the
         // geometry / copy streams of the pipelined loop body (at the lowest priority the full
         // per-frame path dropped from 7.3 k to 5.4 k stereo frames/s), and the scale-space stream
-        // at the highest priority measured within noise
-#if VO_FEAT_CU_Q > 0
-        // experiment: CU-masked streams -- the feature stream (sub[1]) on VO_FEAT_CU_Q quarters of
-        // the CUs (bit i set when i % 4 < Q, an even spread whatever the CU numbering), the scale
-        // space on all CUs or (VO_SS_CU_EXCL) on the complement
-        if (k < 2) {
-            int dev = 0;
-            hipGetDevice(&dev);
-            int n_cu = 0;
-            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-            uint32_t mask[16] = {};
-            const int nw = (n_cu + 31) / 32;
-            for (int i = 0; i < n_cu && i < 512; ++i) {
-                const bool feat = (i % 4) < VO_FEAT_CU_Q;
-                if (k == 1 ? feat : (!VO_SS_CU_EXCL || !feat)) mask[i / 32] |= 1u << (i % 32);
-            }
-            e = hipExtStreamCreateWithCUMask(&c->sub[k], (uint32_t)nw, mask);
-        } else
-            e = hipStreamCreateWithFlags(&c->sub[k], hipStreamNonBlocking);
-#else
+        // at the highest priority measured within noise.  No CU masks: partitioning the CUs
+        // between the two streams measured within noise
         e = hipStreamCreateWithFlags(&c->sub[k], hipStreamNonBlocking);
-#endif
         if (e != hipSuccess) return bail("stream", e);
         if ((e = hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
     }
