@@ -346,6 +346,9 @@ __device__ inline int xcd_remap(int bid, int n)
     return xcd < rm ? xcd * (q + 1) + idx : rm * (q + 1) + (xcd - rm) * q + idx;
 }
 
+#ifndef VO_BS_TAIL_GUARD
+#define VO_BS_TAIL_GUARD 1
+#endif
 #define BS_P 4            // prefetch depth (rows); 6 for the octave-0 base measured the same
 
 // Scale-space kernels raise their wave priority.  The feature stream's kernels (k_desc,
@@ -577,7 +580,7 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                 for (int i = 0; i < CPL * NQ; ++i) w[i] = 0.0f;
                 vec_t vm, vh;
                 fetch(uc, kk, vm, vh);
-                VO_BS_LOAD(kk + P, u);
+                if (!VO_BS_TAIL_GUARD || kk + P < F + TH) VO_BS_LOAD(kk + P, u);   // no prefetch past the band's last row
                 vo_dpp_window<RAD, CPL>(vm, w);
             } else {
                 float* const row = rb;
@@ -588,7 +591,7 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                     *reinterpret_cast<vec_t*>(hpos >= 0 ? row + hpos : dummy) = vh;
                 }
                 __syncthreads();                          // one-wave block: orders the LDS row only
-                VO_BS_LOAD(kk + P, u);
+                if (!VO_BS_TAIL_GUARD || kk + P < F + TH) VO_BS_LOAD(kk + P, u);   // no prefetch past the band's last row
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const vec_t t = (TAG & 32) ? (q & 1 ? vh : vm) : *reinterpret_cast<const vec_t*>(row + CPL * lane + CPL * q);
@@ -811,7 +814,7 @@ __device__ __forceinline__ void decode_word(const Pyramid* __restrict__ py, int 
 // block (val included) <=> val >= all 26 neighbours.  The two ballots per (row,
 // layer) are the strip's even- and odd-column words (bit l = column xs+2l+c);
 // k_seg_emit interleaves each pair back into column order.  Input rows are
-// prefetched 3 rows ahead.
+// prefetched 3 rows ahead; lanes past the plane's last column (row padding) load nothing.
 // ---------------------------------------------------------------------------
 
 // whole-wave lane shifts on the VALU (GFX9 DPP wave_shr:1 / wave_shl:1) instead of
@@ -873,7 +876,7 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
         const int y_ = min(r0 - 1 + (T), rows - 1);                                                \
         const float* rp_ = base + (size_t)y_ * pitch;                                              \
         _Pragma("unroll") for (int lv = 0; lv < NG; ++lv) {                                        \
-            pm[SL][lv] = *reinterpret_cast<const f2_t*>(rp_ + goff[lv] + xa);                     \
+            if (xa < cols) pm[SL][lv] = *reinterpret_cast<const f2_t*>(rp_ + goff[lv] + xa);      \
             ph[SL][lv] = rp_[goff[lv] + hx];                                                       \
         }                                                                                          \
     } while (0)
@@ -888,7 +891,9 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
             d[lv] = pm[SL][lv + 1] - pm[SL][lv];
             hd[lv] = ph[SL][lv + 1] - ph[SL][lv];
         }
-        VO_ET_LOAD(t + W, SL);                        // refill the slot with row t+3
+        // refill the slot with row t+3 -- only rows the band uses (r0-1 .. r0+nrow): the last
+        // steps' prefetches were 3 wasted rows per 30-row band (~9 % of the kernel's fetches)
+        if (t + W <= nrow + 1) VO_ET_LOAD(t + W, SL);
 #pragma unroll
         for (int lv = 0; lv < ND; ++lv) {
             // outer neighbours: xa-1 = lane l-1's xb (lane 0: its halo xs-1), xb+1 = lane
