@@ -458,18 +458,10 @@ __device__ __forceinline__ vo_f4 up4_from_words(uint32_t a0, uint32_t a1, uint32
 #endif
 }
 
-// Per-row hooks of the streaming blur (k_ext_fold runs the extremum test on the rows the last
-// level blur produces); the plain blur uses the empty one.
-struct VoNoHook {
-    template <typename W> __device__ __forceinline__ void row(int, const W&) {}
-    __device__ __forceinline__ void begin() {}
-    template <typename U, typename G> __device__ __forceinline__ void out(U, int, int, const G&) {}
-};
-
-template <int RAD, bool EDGE, int TAG, int CPL, typename HK = VoNoHook>
+template <int RAD, bool EDGE, int TAG, int CPL>
 __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, int pitch, int R, int C,
                                                  float* __restrict__ g_out, const Kern& K,
-                                                 int x0, int y0, int TH, float* rb, const U8Src& u8, HK hk = HK())
+                                                 int x0, int y0, int TH, float* rb, const U8Src& u8)
 {
     // CPL columns per lane (4: 256-column strips, 16-B accesses; 2: 128-column strips,
     // 8-B accesses, half the ring registers -> more waves for the smaller octaves)
@@ -632,7 +624,6 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                     }
                 H[2 * RAD + u][c] = acc;
             }
-            hk.row(kk, w);
             if constexpr (decltype(store_c)::value) {
                 vec_t g;
 #pragma unroll
@@ -653,7 +644,6 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                     if (TAG & 2) *reinterpret_cast<vec_t*>(g_out + off) = g;        // cached store variant
                     else __builtin_nontemporal_store(g, reinterpret_cast<vec_t*>(g_out + off));
                 }
-                hk.out(uc, kk, y0 + kk - F, g);
             }
             if constexpr (!XCH) __syncthreads();
         });
@@ -666,7 +656,6 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
     vo_static_for<P>([&](auto uc) { VO_BS_LOAD(decltype(uc)::value, decltype(uc)::value); });
 #pragma unroll 1
     for (int kk0 = 0; kk0 < F; kk0 += P) block(kk0, std::false_type{});          // ring fill
-    hk.begin();
 #pragma unroll 1
     for (int kk0 = F; kk0 < F + TH; kk0 += P) block(kk0, std::true_type{});      // TH % P == 0
 #undef VO_BS_LOAD
@@ -842,15 +831,15 @@ __device__ __forceinline__ float vo_wave_shl1_or(float old, float x)   // lane i
 
 template <int L>
 __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ py, const float* __restrict__ arena,
-                                                   unsigned long long* __restrict__ mask, float thr, int n_img, int u_base)
+                                                   unsigned long long* __restrict__ mask, float thr, int n_img)
 {
     vo_ss_prio();
     constexpr int NG = L + 3, ND = L + 2, W = 3;      // Gaussian levels, DoG levels, row window
     const int lane = threadIdx.x;
     const int u_all = xcd_remap(blockIdx.x, gridDim.x);
-    const int nu = py->n_units - u_base;              // units from u_base on (octaves not folded)
+    const int nu = py->n_units;
     const int img = u_all / nu;
-    int u = u_all - img * nu + u_base;
+    int u = u_all - img * nu;
     int o = 0;
     while (o + 1 < py->n_oct && py->ebase[o + 1] <= u) ++o;
     o = __builtin_amdgcn_readfirstlane(o);
@@ -958,173 +947,6 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
         step(t0 + 2, std::integral_constant<int, 1>{}, std::true_type{});
     }
 #undef VO_ET_LOAD
-}
-
-// ---------------------------------------------------------------------------
-// Last level blur + extremum test in one pass (large octaves).  The streaming blur of
-// G_{L+1} -> G_{L+2} (2 columns per lane, 128-column strips = the extremum test's strips)
-// hands each G_{L+2} row it produces to FoldHook, which loads G_0 .. G_{L+1} of that row,
-// forms the L+2 DoG rows and runs k_ext_stream's 26-neighbour test one row behind.  The
-// extremum test then never re-reads G_{L+2} (still written: k_refine reads D_{L+1}) and the
-// level blur's input row is the test's G_{L+1}: 12 -> 4 B per octave pixel of traffic for
-// the top level.  G_{L+2} at the strip's halo columns xs-1 / xs+128 (lanes 0 / 63) comes
-// from a scalar row pass of the staged row (same operation order as the packed pass) kept
-// in a 32-row LDS ring, and the matching scalar column pass.  The vertical 3x3x3 maximum is
-// carried as a running pair maximum (rows y-1, y) + the current row.
-// ---------------------------------------------------------------------------
-#ifndef VO_EXT_FOLD
-#define VO_EXT_FOLD 1
-#endif
-template <int RAD, int L>
-struct FoldHook {
-    static constexpr int NGL = L + 2;                // Gaussian levels loaded: G_0 .. G_{L+1}
-    static constexpr int RH = bs_rh(RAD, 2);
-    typedef float f2_t __attribute__((ext_vector_type(2)));
-    const float* base;                               // image arena
-    size_t goff[NGL];
-    int pitch, R, C, y0, TH, x0, xl, hxl, lane, strip, wr;
-    float thr;
-    float k[RAD + 1];                                // blur taps
-    float* xr;                                       // LDS ring [2][32]: halo-column row passes
-    unsigned long long* mrow;
-    int wb[L];
-    bool in0, in1;
-    f2_t gq[2][NGL];                                 // prefetched G_0..G_{L+1} rows (2 slots)
-    float gh[2][NGL];                                //   and their halo column
-    f2_t pmx[L], pmn[L], mx[L], mn[L], dcp[L];       // pair max/min (rows y-1, y), last row's, centres
-
-    __device__ __forceinline__ void load(int slot_is_1, int y)
-    {
-        const float* rp = base + (size_t)y * pitch;
-#pragma unroll
-        for (int l = 0; l < NGL; ++l) {
-            f2_t v = f2_t{0.0f, 0.0f};
-            if (xl < C) v = *reinterpret_cast<const f2_t*>(rp + goff[l] + xl);
-            const float h = rp[goff[l] + hxl];
-            if (slot_is_1) { gq[1][l] = v; gh[1][l] = h; } else { gq[0][l] = v; gh[0][l] = h; }
-        }
-    }
-    template <typename W> __device__ __forceinline__ void row(int kk, const W& w)
-    {
-        // row pass at the halo columns: lane 0 -> xs-1 (window index RH-1), lane 63 -> xs+128 (RH+2)
-        float a = k[0] * w[RH - 1], b = k[0] * w[RH + 2];
-#pragma unroll
-        for (int j = 1; j <= RAD; ++j) {
-            a = __builtin_fmaf(k[j], w[RH - 1 - j] + w[RH - 1 + j], a);
-            b = __builtin_fmaf(k[j], w[RH + 2 - j] + w[RH + 2 + j], b);
-        }
-        if (lane == 0) xr[kk & 31] = a;
-        if (lane == 63) xr[32 + (kk & 31)] = b;
-    }
-    __device__ __forceinline__ void begin()
-    {
-        load(0, y0);
-        load(1, y0 + 1);
-    }
-    template <typename U, typename GV> __device__ __forceinline__ void out(U uc, int kk, int y, const GV& g)
-    {
-        constexpr int SL = decltype(uc)::value & 1;  // output step y - y0 = u (mod 4): static slot
-        const int s = y - y0;
-        // G_{L+2} at this lane's halo column (meaningful in lanes 0 and 63)
-        const float* xq = xr + (lane == 63 ? 32 : 0);
-        float g5h = k[0] * xq[(kk - RAD) & 31];
-#pragma unroll
-        for (int j = 1; j <= RAD; ++j) g5h = __builtin_fmaf(k[j], xq[(kk - RAD - j) & 31] + xq[(kk - RAD + j) & 31], g5h);
-        f2_t Gv[NGL + 1];
-        float Hh[NGL + 1];
-#pragma unroll
-        for (int l = 0; l < NGL; ++l) { Gv[l] = gq[SL][l]; Hh[l] = gh[SL][l]; }
-        Gv[NGL] = f2_t{g.x, g.y};
-        Hh[NGL] = g5h;
-        if (y + 2 < y0 + TH) load(SL, y + 2);        // refill this slot with row y+2
-        constexpr int ND = L + 2;
-        f2_t d[ND], hmx[ND], hmn[ND];
-#pragma unroll
-        for (int lv = 0; lv < ND; ++lv) {
-            d[lv] = Gv[lv + 1] - Gv[lv];
-            const float hd = Hh[lv + 1] - Hh[lv];
-            const float la = vo_wave_shr1_or(hd, d[lv].y), rb = vo_wave_shl1_or(hd, d[lv].x);
-            hmx[lv] = f2_t{fmaxf(fmaxf(la, d[lv].x), d[lv].y), fmaxf(fmaxf(d[lv].x, d[lv].y), rb)};
-            hmn[lv] = f2_t{fminf(fminf(la, d[lv].x), d[lv].y), fminf(fminf(d[lv].x, d[lv].y), rb)};
-        }
-        f2_t cx[L], cn[L];                            // this row's 3-level x 3-column max / min per layer
-#pragma unroll
-        for (int l = 0; l < L; ++l) {
-            cx[l] = f2_t{fmaxf(fmaxf(hmx[l].x, hmx[l + 1].x), hmx[l + 2].x), fmaxf(fmaxf(hmx[l].y, hmx[l + 1].y), hmx[l + 2].y)};
-            cn[l] = f2_t{fminf(fminf(hmn[l].x, hmn[l + 1].x), hmn[l + 2].x), fminf(fminf(hmn[l].y, hmn[l + 1].y), hmn[l + 2].y)};
-        }
-        const int yt = y - 1;                         // tested row: needs rows y-2 .. y
-        if (s >= 2 && yt >= VO_SIFT_BORDER && yt < R - VO_SIFT_BORDER) {
-#pragma unroll
-            for (int l = 0; l < L; ++l) {
-                bool e[2];
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    const float val = c ? dcp[l].y : dcp[l].x;
-                    const float bmx = fmaxf(c ? pmx[l].y : pmx[l].x, c ? cx[l].y : cx[l].x);
-                    const float bmn = fminf(c ? pmn[l].y : pmn[l].x, c ? cn[l].y : cn[l].x);
-                    e[c] = ((val > thr) & (val >= bmx)) | ((val < -thr) & (val <= bmn));
-                }
-                const uint64_t w0 = __ballot(e[0] & in0), w1 = __ballot(e[1] & in1);
-                const int kw = 2 * strip + lane;
-                if (lane < 2 && kw < wr) mrow[wb[l] + (size_t)(yt - VO_SIFT_BORDER) * wr + kw] = lane ? w1 : w0;
-            }
-        }
-#pragma unroll
-        for (int l = 0; l < L; ++l) {
-            if (s >= 1) {
-                pmx[l] = f2_t{fmaxf(mx[l].x, cx[l].x), fmaxf(mx[l].y, cx[l].y)};
-                pmn[l] = f2_t{fminf(mn[l].x, cn[l].x), fminf(mn[l].y, cn[l].y)};
-            }
-            mx[l] = cx[l];
-            mn[l] = cn[l];
-            dcp[l] = d[l + 1];
-        }
-    }
-};
-
-template <int RAD, int L>
-__global__ __launch_bounds__(64, 2) void k_ext_fold(const Pyramid* __restrict__ py, float* __restrict__ arena,
-                                                 unsigned long long* __restrict__ mask, float thr, Kern K, int o,
-                                                 int n_strips, int n_bands, int TH)
-{
-    vo_ss_prio();
-    constexpr int CPL = 2, RH = bs_rh(RAD, CPL);
-    __shared__ __attribute__((aligned(16))) float rb[bs_rw(RAD, CPL) + 64 * CPL];
-    __shared__ float xr[64];
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int strip = bid % n_strips, tb = bid / n_strips;
-    const int band = tb % n_bands, img = tb / n_bands;
-    const OctGeom& g = py->oct[o];
-    const int R = g.rows, C = g.cols, pitch = g.pitch;
-    const int x0 = strip * 64 * CPL, y0 = min(band * (TH - 2), R - TH);
-    const float* base = arena + img * py->istride;
-    FoldHook<RAD, L> hk;
-    hk.base = base;
-#pragma unroll
-    for (int l = 0; l < L + 2; ++l) hk.goff[l] = g.g_off[l];
-    hk.pitch = pitch; hk.R = R; hk.C = C; hk.y0 = y0; hk.TH = TH; hk.x0 = x0;
-    hk.lane = threadIdx.x;
-    hk.xl = x0 + 2 * (int)threadIdx.x;
-    hk.hxl = threadIdx.x == 63 ? min(x0 + 128, C - 1) : max(x0 - 1, 0);
-    hk.strip = strip;
-    hk.wr = py->wrow[o];
-    hk.thr = thr;
-#pragma unroll
-    for (int j = 0; j <= RAD; ++j) hk.k[j] = K.k[j];
-    hk.xr = xr;
-    hk.mrow = mask + (size_t)img * py->n_words;
-#pragma unroll
-    for (int l = 0; l < L; ++l) hk.wb[l] = py->wbase[o * L + l];
-    hk.in0 = hk.xl >= VO_SIFT_BORDER && hk.xl < C - VO_SIFT_BORDER;
-    hk.in1 = hk.xl + 1 >= VO_SIFT_BORDER && hk.xl + 1 < C - VO_SIFT_BORDER;
-    const float* src = base + g.g_off[L + 1];
-    float* dst = arena + img * py->istride + g.g_off[L + 2];
-    const U8Src u8{nullptr, 0, 0, 0};
-    if (x0 - RH < 0 || x0 + 64 * CPL + RH > C)
-        blur_stream_body<RAD, true, 0, CPL, FoldHook<RAD, L>&>(src, pitch, R, C, dst, K, x0, y0, TH, rb, u8, hk);
-    else
-        blur_stream_body<RAD, false, 0, CPL, FoldHook<RAD, L>&>(src, pitch, R, C, dst, K, x0, y0, TH, rb, u8, hk);
 }
 
 // Block-wide exclusive scan of one value per thread (1024 threads).
@@ -1909,8 +1731,6 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
 {
     const int L = py.L;
     float* A = b.arena;
-    const float thr = (float)floor(0.5 * p.contrast_threshold / L * 255.0);
-    int n_fold = 0;                                  // octaves 0 .. n_fold-1 built + tested by k_ext_fold
     // first octave from which every remaining octave fits the one-launch LDS path
     int o_small = py.n_oct, small_rtab = 0;
     size_t small_lds = 0;
@@ -1966,35 +1786,21 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
             VO_LAUNCH(k_down, dim3((C + 255) / 256, R, n_img), dim3(256), 0, s, A + pg.g_off[L], py.istride, pg.pitch,
                       A + g.g_off[0], py.istride, g.pitch, C);
         }
-        // the top level of a large octave is built by k_ext_fold together with the octave's
-        // extremum test (a prefix of the octaves: k_ext_stream takes the rest in one launch)
-        const bool fold = VO_EXT_FOLD && o == n_fold && L == 3 && py.krad[L + 2] == 13 && R >= 64 && py.wrow[o] > 0;
-        for (int i = 1; i < L + (fold ? 2 : 3); ++i) {
+        for (int i = 1; i < L + 3; ++i) {
             Kern K = make_kern(py, i);
             launch_blur<0>(gf, s, A + g.g_off[i - 1], py.istride, py.istride, g.pitch, R, C, A + g.g_off[i], nullptr, K, src,
                            0, 0);
         }
-        if (fold) {
-            // bands of TH G rows overlapping by 2 (each tests its TH-2 interior rows)
-#ifndef VO_FOLD_TH
-#define VO_FOLD_TH 128
-#endif
-            const int TH = std::min(VO_FOLD_TH, R / BS_P * BS_P);
-            const int n_strips = (C + 127) / 128, n_bands = (R - 2 + TH - 3) / (TH - 2);
-            VO_LAUNCH_NAMED("k_ext_fold", (k_ext_fold<13, 3>), dim3(n_strips * n_bands * n_img), dim3(64), 0, s, d_py, A,
-                            b.mask, thr, make_kern(py, L + 2), o, n_strips, n_bands, TH);
-            ++n_fold;
-        }
     }
-    const int u_base = py.ebase[n_fold];
-    if (py.n_units > u_base) {
-        const dim3 ge((py.n_units - u_base) * n_img);
+    const float thr = (float)floor(0.5 * p.contrast_threshold / L * 255.0);
+    if (py.n_units > 0) {
+        const dim3 ge(py.n_units * n_img);
         switch (L) {
-        case 1: VO_LAUNCH(k_ext_stream<1>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_base); break;
-        case 2: VO_LAUNCH(k_ext_stream<2>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_base); break;
-        case 3: VO_LAUNCH(k_ext_stream<3>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_base); break;
-        case 4: VO_LAUNCH(k_ext_stream<4>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_base); break;
-        default: VO_LAUNCH(k_ext_stream<5>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_base); break;
+        case 1: VO_LAUNCH(k_ext_stream<1>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
+        case 2: VO_LAUNCH(k_ext_stream<2>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
+        case 3: VO_LAUNCH(k_ext_stream<3>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
+        case 4: VO_LAUNCH(k_ext_stream<4>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
+        default: VO_LAUNCH(k_ext_stream<5>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
         }
     }
 }
