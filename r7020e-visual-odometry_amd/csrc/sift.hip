@@ -346,9 +346,6 @@ __device__ inline int xcd_remap(int bid, int n)
     return xcd < rm ? xcd * (q + 1) + idx : rm * (q + 1) + (xcd - rm) * q + idx;
 }
 
-#ifndef VO_BS_TAIL_GUARD
-#define VO_BS_TAIL_GUARD 1
-#endif
 #define BS_P 4            // prefetch depth (rows); 6 for the octave-0 base measured the same
 
 // Scale-space kernels raise their wave priority.  The feature stream's kernels (k_desc,
@@ -367,21 +364,17 @@ __host__ __device__ constexpr int bs_rh(int r, int cpl) { return (r + cpl - 1) /
 __host__ __device__ constexpr int bs_rw(int r, int cpl) { return 64 * cpl + 2 * bs_rh(r, cpl); }
 // Row-window exchange of the streaming blur.  Each lane holds CPL consecutive columns of the
 // input row; the row pass needs r columns either side.  Halo-lane layout (bs_hl: 4-column lanes,
-// r <= VO_BLUR_DPP_MAXR): the wave covers 64*CPL input columns starting RH left of its output
+// r <= kBlurDppMaxR): the wave covers 64*CPL input columns starting RH left of its output
 // strip, its outer RH/CPL lanes each side hold only halo columns and store nothing, and the
 // neighbours' columns arrive by whole-wave DPP shifts (wave_shr:1 / wave_shl:1, one VALU op
 // per column per level).  No halo loads, no halo upsampling, no LDS round trip: per row the
 // LDS exchange cost 2 ds_write_b128 (13 LDS cycles each, at half rate from one wave) + (1 +
 // 2 rh/4) ds_read_b128, which base_probe measured at ~180 of the octave-0 base kernel's ~430 us.
-#ifndef VO_BLUR_DPP_MAXR
-#define VO_BLUR_DPP_MAXR 5
-#endif
-#ifndef VO_BLUR_DPP_BASE_ONLY
-#define VO_BLUR_DPP_BASE_ONLY 0
-#endif
+// (r >= 6, and the r = 5 level with 2-column lanes, keep the LDS exchange: measured faster)
+constexpr int kBlurDppMaxR = 5;
 __host__ __device__ constexpr bool bs_hl(int r, int cpl, int tag)
 {
-    return cpl == 4 && r <= VO_BLUR_DPP_MAXR && !(tag & 32) && (!VO_BLUR_DPP_BASE_ONLY || (tag & 1));
+    return cpl == 4 && r <= kBlurDppMaxR && !(tag & 32);
 }
 // output columns per strip
 __host__ __device__ constexpr int bs_sw(int r, int cpl, int tag) { return 64 * cpl - (bs_hl(r, cpl, tag) ? 2 * bs_rh(r, cpl) : 0); }
@@ -421,9 +414,6 @@ __device__ __forceinline__ void vo_dpp_window(const vec_t& vm, float* w)
 }
 
 
-#ifndef VO_UP_DOT4
-#define VO_UP_DOT4 1
-#endif
 // u8 source of the octave-0 base level (TAG & 4): the x2 upsample is formed
 // while staging each input row, from raw source words prefetched like floats.
 struct U8Src { const uint8_t* p; int ld, rows, cols; };
@@ -432,7 +422,6 @@ __device__ __forceinline__ vo_f4 up4_from_words(uint32_t a0, uint32_t a1, uint32
 {
     // 4 source bytes (columns g2-1 .. g2+2) of rows ya, yb -> outputs x .. x+3 (x = 2*g2), as up_sample
     const uint32_t ba = __builtin_amdgcn_alignbyte(a1, a0, sa), bb = __builtin_amdgcn_alignbyte(b1, b0, sb);
-#if VO_UP_DOT4
     // up_sample's 0.75 ha + 0.25 hb, ha = 0.75 a + 0.25 b, is exact in fp32 for bytes (every
     // partial is a multiple of 1/16 below 256), so it equals (9 A[xa] + 3 A[xb] + 3 B[xa] +
     // B[xb]) / 16: one byte permute + one v_dot4_u32_u8 per output instead of ~10 VALU.
@@ -445,17 +434,6 @@ __device__ __forceinline__ vo_f4 up4_from_words(uint32_t a0, uint32_t a1, uint32
         r[i] = (float)__builtin_amdgcn_udot4(q, 0x01030309u, 0u, false) * 0.0625f;
     }
     return vo_f4{r[0], r[1], r[2], r[3]};
-#else
-    float r[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int xa = 1 + (i >> 1), xb = (i & 1) ? xa + 1 : xa - 1;
-        const float ha = 0.75f * (float)((ba >> (8 * xa)) & 0xff) + 0.25f * (float)((ba >> (8 * xb)) & 0xff);
-        const float hb = 0.75f * (float)((bb >> (8 * xa)) & 0xff) + 0.25f * (float)((bb >> (8 * xb)) & 0xff);
-        r[i] = 0.75f * ha + 0.25f * hb;
-    }
-    return vo_f4{r[0], r[1], r[2], r[3]};
-#endif
 }
 
 template <int RAD, bool EDGE, int TAG, int CPL>
@@ -580,7 +558,7 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                 for (int i = 0; i < CPL * NQ; ++i) w[i] = 0.0f;
                 vec_t vm, vh;
                 fetch(uc, kk, vm, vh);
-                if (!VO_BS_TAIL_GUARD || kk + P < F + TH) VO_BS_LOAD(kk + P, u);   // no prefetch past the band's last row
+                if (kk + P < F + TH) VO_BS_LOAD(kk + P, u);   // no prefetch past the band's last row
                 vo_dpp_window<RAD, CPL>(vm, w);
             } else {
                 float* const row = rb;
@@ -591,7 +569,7 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                     *reinterpret_cast<vec_t*>(hpos >= 0 ? row + hpos : dummy) = vh;
                 }
                 __syncthreads();                          // one-wave block: orders the LDS row only
-                if (!VO_BS_TAIL_GUARD || kk + P < F + TH) VO_BS_LOAD(kk + P, u);   // no prefetch past the band's last row
+                if (kk + P < F + TH) VO_BS_LOAD(kk + P, u);   // no prefetch past the band's last row
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const vec_t t = (TAG & 32) ? (q & 1 ? vh : vm) : *reinterpret_cast<const vec_t*>(row + CPL * lane + CPL * q);
@@ -1425,9 +1403,6 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
 // u32 fixed point (vo_desc_fx_quant) sums are order-free, so the copies are folded after
 // the loop without changing a bit.
 #define DCS 324
-#ifndef VO_DESC_ROW3
-#define VO_DESC_ROW3 1
-#endif
 template <int DCOPIES>
 __global__ __launch_bounds__(64, 5) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                              const KpInt* __restrict__ kpi, const int* __restrict__ n_kp,
@@ -1552,14 +1527,10 @@ __global__ __launch_bounds__(64, 5) void k_desc(const Pyramid* __restrict__ py, 
 #pragma unroll
             for (int u = 0; u < U; ++u) {                // phase 1b: all gradient loads in flight together
                 const float* gp = gim + off[u];           // (every listed sample is valid)
-#if VO_DESC_ROW3
                 // the row neighbours x-1 .. x+1 as one 12-B load: 3 loads per sample instead of 4
                 typedef float f3_t __attribute__((ext_vector_type(3)));
                 const f3_t h = *reinterpret_cast<const f3_t*>(gp - 1);
                 g4[u][0] = h.z; g4[u][1] = h.x;
-#else
-                g4[u][0] = gp[1]; g4[u][1] = gp[-1];
-#endif
                 g4[u][2] = gp[-(ptrdiff_t)P]; g4[u][3] = gp[P];
             }
 #pragma unroll
