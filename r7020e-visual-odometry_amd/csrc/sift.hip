@@ -1768,6 +1768,22 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
                            0, 0);
         }
     }
+}
+
+// grid of the wave-per-keypoint kernels (grid-stride over the flat keypoint space):
+// 32768 one-wave workgroups (~7 keypoints each at 64 frames x ~1.8k): shorter tail than
+// 8192 (k_desc 2.25 -> 2.05 ms, k_orient 0.77 -> 0.67 ms isolated) and workgroups turn over
+// often enough for the scale-space stream's blurs to get slots while they run
+constexpr int kFeatureGrid = 32768;
+
+// The extremum test runs at the head of the feature stages, not at the tail of the scale
+// space: the scale-space stream is the pipeline's critical path (7.1 of 7.9 ms per 64-frame
+// step in situ, against 4.7 ms of feature stages), so the test's 1.7 ms balance the streams.
+static void sift_enqueue_extrema(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
+                                 const Pyramid* d_py)
+{
+    const int L = py.L;
+    float* A = b.arena;
     const float thr = (float)floor(0.5 * p.contrast_threshold / L * 255.0);
     if (py.n_units > 0) {
         const dim3 ge(py.n_units * n_img);
@@ -1781,15 +1797,10 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
     }
 }
 
-// grid of the wave-per-keypoint kernels (grid-stride over the flat keypoint space):
-// 32768 one-wave workgroups (~7 keypoints each at 64 frames x ~1.8k): shorter tail than
-// 8192 (k_desc 2.25 -> 2.05 ms, k_orient 0.77 -> 0.67 ms isolated) and workgroups turn over
-// often enough for the scale-space stream's blurs to get slots while they run
-constexpr int kFeatureGrid = 32768;
-
 void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
                            const Pyramid* d_py)
 {
+    sift_enqueue_extrema(py, b, n_img, p, s, d_py);
     float* A = b.arena;
     const dim3 gs(py.n_seg > 0 ? py.n_seg : 1, n_img);
     VO_LAUNCH(k_seg_count, gs, dim3(256), 0, s, b.mask, b.woff, py.n_words, py.n_seg);

@@ -149,8 +149,8 @@ void sift_free(SiftBuffers& b);
 // d_py is a device copy of py.
 void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img,
                   const vo_sift_params& p, hipStream_t s, const Pyramid* d_py);
-// The two phases of sift_enqueue: the bandwidth-bound scale space + extremum masks, and the
-// latency-bound feature stages (compaction, refinement, orientation, descriptors).
+// The two phases of sift_enqueue: the scale space (base, level blurs, octave bases), and the
+// feature stages (extremum masks, compaction, refinement, orientation, descriptors).
 void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img,
                           const vo_sift_params& p, hipStream_t s, const Pyramid* d_py);
 void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
