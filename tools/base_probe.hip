@@ -18,19 +18,34 @@ void Profiler::reset_totals() {}
 Profiler::~Profiler() {}
 }
 
-template <int P>
+// MODE 0: strips of sw columns (sw = 256: aligned 1-KB row segments; 240: the base kernel's
+// halo-lane strips, 960-B segments that start mid-line for every other strip), XCD-contiguous
+// ids, strip fastest, non-temporal stores; 1: no XCD remap; 2: plain stores; 3: each wave writes
+// TH KB of contiguous bytes instead (same total, bounded to the buffer)
+template <int MODE>
 __global__ __launch_bounds__(64) void k_store_strip(float* __restrict__ b, int pitch, int R, size_t plane, int n_strips,
-                                                    int n_bands, int TH)
+                                                    int n_bands, int TH, int sw, size_t cap_f4)
 {
     typedef float f4 __attribute__((ext_vector_type(4)));
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bid = MODE == 1 ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+    if (MODE == 3) {
+        const size_t first = (size_t)bid * TH * 64;
+        if (first + (size_t)TH * 64 > cap_f4) return;
+        f4* p = reinterpret_cast<f4*>(b) + first + threadIdx.x;
+        const f4 v = {1.0f, 2.0f, 3.0f, (float)bid};
+        for (int k = 0; k < TH; ++k) __builtin_nontemporal_store(v, p + (size_t)k * 64);
+        return;
+    }
     const int strip = bid % n_strips, tb = bid / n_strips, band = tb % n_bands, img = tb / n_bands;
-    const int x0 = strip * 256, y0 = min(band * TH, R - TH);
+    const int x0 = strip * sw, y0 = min(band * TH, R - TH);
     const int xl = x0 + 4 * (int)threadIdx.x;
+    if (4 * (int)threadIdx.x >= sw || xl + 4 > pitch) return;
     float* bp = b + img * plane;
     const f4 v = {1.0f, 2.0f, 3.0f, (float)img};
-    for (int k = 0; k < TH; ++k)
-        __builtin_nontemporal_store(v, reinterpret_cast<f4*>(bp + (size_t)(y0 + k) * pitch + xl));
+    for (int k = 0; k < TH; ++k) {
+        f4* q = reinterpret_cast<f4*>(bp + (size_t)(y0 + k) * pitch + xl);
+        if (MODE == 2) *q = v; else __builtin_nontemporal_store(v, q);
+    }
 }
 
 template <int TAG>
@@ -71,18 +86,34 @@ int main()
     K.r = 5;
     for (int j = 0; j <= 5; ++j) K.k[j] = 1.0f / 11;
     const double gb = 4.0 * R * C * n / 1e9;
-    for (int TH : {32, 64, 128, 256}) {
-        const int n_strips = (C + 255) / 256, n_bands = (R + TH - 1) / TH;
+    auto store_only = [&](auto kern, int TH, int sw) {
+        const int n_strips = (C + sw - 1) / sw, n_bands = (R + TH - 1) / TH;
+        const size_t cap = plane * n / 4;
         hipEvent_t a, b;
         hipEventCreate(&a); hipEventCreate(&b);
-        hipLaunchKernelGGL(k_store_strip<4>, dim3(n_strips * n_bands * n), dim3(64), 0, 0, dst, pitch, R, plane, n_strips, n_bands, TH);
+        hipLaunchKernelGGL(kern, dim3(n_strips * n_bands * n), dim3(64), 0, 0, dst, pitch, R, plane, n_strips, n_bands, TH, sw, cap);
         hipEventRecord(a);
         for (int i = 0; i < 10; ++i)
-            hipLaunchKernelGGL(k_store_strip<4>, dim3(n_strips * n_bands * n), dim3(64), 0, 0, dst, pitch, R, plane, n_strips, n_bands, TH);
+            hipLaunchKernelGGL(kern, dim3(n_strips * n_bands * n), dim3(64), 0, 0, dst, pitch, R, plane, n_strips, n_bands, TH, sw, cap);
         hipEventRecord(b);
         hipEventSynchronize(b);
         float ms;
         hipEventElapsedTime(&ms, a, b);
+        return 100.0f * ms;     // us per launch
+    };
+    for (int TH : {64, 128}) {
+        const int nb = (R + TH - 1) / TH;
+        auto gbs = [&](int sw) { return 4.0 * sw * TH * ((C + sw - 1) / sw) * nb * n / 1e9; };   // bytes the strip stores write
+        const float m0 = store_only(k_store_strip<0>, TH, 256), m1 = store_only(k_store_strip<1>, TH, 256);
+        const float m2 = store_only(k_store_strip<2>, TH, 256), m3 = store_only(k_store_strip<3>, TH, 256);
+        const float m4 = store_only(k_store_strip<0>, TH, 240), m5 = store_only(k_store_strip<0>, TH, 224);
+        const float m6 = store_only(k_store_strip<2>, TH, 240);
+        printf("TH %3d store-only TB/s: 256-col strips %5.2f | no XCD remap %5.2f | plain stores %5.2f | contiguous %5.2f | "
+               "240-col %5.2f | 224-col %5.2f | 240-col plain %5.2f\n", TH, gbs(256) / m0 * 1e3, gbs(256) / m1 * 1e3,
+               gbs(256) / m2 * 1e3, gbs(256) / m3 * 1e3, gbs(240) / m4 * 1e3, gbs(224) / m5 * 1e3, gbs(240) / m6 * 1e3);
+    }
+    for (int TH : {32, 64, 128, 256}) {
+        const float ms = store_only(k_store_strip<0>, TH, 256) / 100.0f;
         const float t0 = run<5>(u8, dst, plane, pitch, R, C, n, TH, K);
         const float t8 = run<5 | 8>(u8, dst, plane, pitch, R, C, n, TH, K);
         const float t24 = run<5 | 24>(u8, dst, plane, pitch, R, C, n, TH, K);
