@@ -21,7 +21,8 @@ Profiler::~Profiler() {}
 // MODE 0: strips of sw columns (sw = 256: aligned 1-KB row segments; 240: the base kernel's
 // halo-lane strips, 960-B segments that start mid-line for every other strip), XCD-contiguous
 // ids, strip fastest, non-temporal stores; 1: no XCD remap; 2: plain stores; 3: each wave writes
-// TH KB of contiguous bytes instead (same total, bounded to the buffer)
+// TH KB of contiguous bytes instead (same total, bounded to the buffer); 16 + n: MODE 0 paced by
+// s_sleep n after every row (the base kernel issues one row store per ~row-pass of work)
 template <int MODE>
 __global__ __launch_bounds__(64) void k_store_strip(float* __restrict__ b, int pitch, int R, size_t plane, int n_strips,
                                                     int n_bands, int TH, int sw, size_t cap_f4)
@@ -45,6 +46,7 @@ __global__ __launch_bounds__(64) void k_store_strip(float* __restrict__ b, int p
     for (int k = 0; k < TH; ++k) {
         f4* q = reinterpret_cast<f4*>(bp + (size_t)(y0 + k) * pitch + xl);
         if (MODE == 2) *q = v; else __builtin_nontemporal_store(v, q);
+        if constexpr (MODE >= 16) __builtin_amdgcn_s_sleep(MODE - 16);   // paced: ~64 (MODE-16) cycles per row
     }
 }
 
@@ -111,6 +113,14 @@ int main()
         printf("TH %3d store-only TB/s: 256-col strips %5.2f | no XCD remap %5.2f | plain stores %5.2f | contiguous %5.2f | "
                "240-col %5.2f | 224-col %5.2f | 240-col plain %5.2f\n", TH, gbs(256) / m0 * 1e3, gbs(256) / m1 * 1e3,
                gbs(256) / m2 * 1e3, gbs(256) / m3 * 1e3, gbs(240) / m4 * 1e3, gbs(224) / m5 * 1e3, gbs(240) / m6 * 1e3);
+    }
+    for (int TH : {64, 128}) {
+        const int nb = (R + TH - 1) / TH;
+        const double g = 4.0 * 256 * TH * ((C + 255) / 256) * nb * n / 1e9;
+        printf("TH %3d paced store-only TB/s: s_sleep 1 %5.2f | 2 %5.2f | 4 %5.2f | 8 %5.2f | 15 %5.2f\n", TH,
+               g / store_only(k_store_strip<17>, TH, 256) * 1e3, g / store_only(k_store_strip<18>, TH, 256) * 1e3,
+               g / store_only(k_store_strip<20>, TH, 256) * 1e3, g / store_only(k_store_strip<24>, TH, 256) * 1e3,
+               g / store_only(k_store_strip<31>, TH, 256) * 1e3);
     }
     for (int TH : {32, 64, 128, 256}) {
         const float ms = store_only(k_store_strip<0>, TH, 256) / 100.0f;
