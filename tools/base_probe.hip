@@ -50,6 +50,36 @@ __global__ __launch_bounds__(64) void k_store_strip(float* __restrict__ b, int p
     }
 }
 
+// throughput-bound VALU work (8 independent FMA chains per lane): its time must scale with the
+// number of CUs a stream may use, which checks that a CU mask is honoured
+__global__ __launch_bounds__(64) void k_valu(float* out, int iters)
+{
+    float a[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = threadIdx.x * 1e-3f + j;
+    for (int i = 0; i < iters; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = __builtin_fmaf(a[j], 1.0001f, 1e-7f);
+    float t = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t += a[j];
+    if (t == 12345.0f) out[blockIdx.x] = t;
+}
+
+static float run_valu(float* out, hipStream_t st)
+{
+    hipEvent_t a, b;
+    hipEventCreate(&a); hipEventCreate(&b);
+    hipLaunchKernelGGL(k_valu, dim3(16384), dim3(64), 0, st, out, 2000);
+    hipEventRecord(a, st);
+    hipLaunchKernelGGL(k_valu, dim3(16384), dim3(64), 0, st, out, 2000);
+    hipEventRecord(b, st);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    return 1000.0f * ms;
+}
+
 template <int TAG>
 static float run(const uint8_t* u8, float* dst, size_t plane, int pitch, int R, int C, int n_img, int TH, const Kern& K,
                  hipStream_t st = 0)
@@ -103,6 +133,20 @@ int main()
         hipEventElapsedTime(&ms, a, b);
         return 100.0f * ms;     // us per launch
     };
+    auto store_only_s = [&](hipStream_t st) {
+        const int TH = 128, n_strips = (C + 255) / 256, n_bands = (R + TH - 1) / TH;
+        hipEvent_t a, b;
+        hipEventCreate(&a); hipEventCreate(&b);
+        hipLaunchKernelGGL(k_store_strip<0>, dim3(n_strips * n_bands * n), dim3(64), 0, st, dst, pitch, R, plane, n_strips, n_bands, TH, 256, (size_t)0);
+        hipEventRecord(a, st);
+        for (int i = 0; i < 10; ++i)
+            hipLaunchKernelGGL(k_store_strip<0>, dim3(n_strips * n_bands * n), dim3(64), 0, st, dst, pitch, R, plane, n_strips, n_bands, TH, 256, (size_t)0);
+        hipEventRecord(b, st);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        return 100.0f * ms;
+    };
     for (int TH : {64, 128}) {
         const int nb = (R + TH - 1) / TH;
         auto gbs = [&](int sw) { return 4.0 * sw * TH * ((C + sw - 1) / sw) * nb * n / 1e9; };   // bytes the strip stores write
@@ -140,7 +184,8 @@ int main()
             if (i % div == 0) m[i / 32] |= 1u << (i % 32);
         hipStream_t st;
         hipExtStreamCreateWithCUMask(&st, (uint32_t)((n_cu + 31) / 32), m);
-        printf("CU mask 1/%d: base %6.1f us (TH 128)\n", div, run<5>(u8, dst, plane, pitch, R, C, n, 128, K, st));
+        printf("CU mask 1/%d: base %6.1f us (TH 128) | store-only %6.1f us | VALU-bound %7.1f us\n", div,
+               run<5>(u8, dst, plane, pitch, R, C, n, 128, K, st), store_only_s(st), run_valu(reinterpret_cast<float*>(u8), st));
     }
     return 0;
 }
