@@ -175,17 +175,22 @@ int main()
         printf("TH %3d: store-only %6.1f us (%5.2f TB/s) | base %6.1f us (%5.2f TB/s) | no-row %6.1f | no row/col %6.1f | "
                "no row/col/LDS %6.1f\n", TH, 100.0f * ms, gb / (100.0f * ms) * 1e3, t0, gb / t0 * 1e3, t8, t24, t56);
     }
-    // the same base kernel on CU-masked streams (bit i set when i % div == 0)
+    // the same kernels on CU-masked streams: interleaved masks (bit i set when i % div == 0) and
+    // contiguous ones (the first n_cu / div bits); the VALU-bound kernel shows whether a mask binds
     int n_cu = 0;
     hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, 0);
-    for (int div : {1, 2, 4, 8}) {
-        uint32_t m[16] = {};
-        for (int i = 0; i < n_cu && i < 512; ++i)
-            if (i % div == 0) m[i / 32] |= 1u << (i % 32);
-        hipStream_t st;
-        hipExtStreamCreateWithCUMask(&st, (uint32_t)((n_cu + 31) / 32), m);
-        printf("CU mask 1/%d: base %6.1f us (TH 128) | store-only %6.1f us | VALU-bound %7.1f us\n", div,
-               run<5>(u8, dst, plane, pitch, R, C, n, 128, K, st), store_only_s(st), run_valu(reinterpret_cast<float*>(u8), st));
-    }
+    printf("CUs %d\n", n_cu);
+    for (int contig = 0; contig < 2; ++contig)
+        for (int div : {1, 2, 4, 8, 64}) {
+            uint32_t m[16] = {};
+            for (int i = 0; i < n_cu && i < 512; ++i)
+                if (contig ? i < n_cu / div : i % div == 0) m[i / 32] |= 1u << (i % 32);
+            hipStream_t st;
+            const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)((n_cu + 31) / 32), m);
+            if (e != hipSuccess) { printf("%s 1/%d: %s\n", contig ? "contiguous" : "interleaved", div, hipGetErrorString(e)); continue; }
+            printf("%s CU mask 1/%d: VALU-bound %7.1f us | base %6.1f us (TH 128) | store-only %6.1f us\n",
+                   contig ? "contiguous" : "interleaved", div, run_valu(reinterpret_cast<float*>(u8), st),
+                   div <= 8 ? run<5>(u8, dst, plane, pitch, R, C, n, 128, K, st) : 0.0f, div <= 8 ? store_only_s(st) : 0.0f);
+        }
     return 0;
 }
