@@ -1,6 +1,8 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-VO_LIBPATH=$GRAFT_REPO_ROOT/tools/variants/cu4x/libvo.so timeout -k 10 300 python -u -m pytest tests/test_gpu_sift_match.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/tests_cu4x.log 2>&1 || { tail -30 gpurun_out/tests_cu4x.log; exit 1; }
-tail -1 gpurun_out/tests_cu4x.log
-bash tools/variant_bench.sh cu4x cu3x cu5x cu4s
+for v in bp2 xp2; do
+  VO_LIBPATH=$GRAFT_REPO_ROOT/tools/variants/$v/libvo.so timeout -k 10 300 python -u -m pytest tests/test_gpu_pyramid.py tests/test_gpu_sift_match.py tests/test_gpu_edge.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/tests_$v.log 2>&1 || { tail -30 gpurun_out/tests_$v.log; exit 1; }
+  echo "$v $(tail -1 gpurun_out/tests_$v.log)"
+done
+bash tools/variant_bench.sh bp2 xp2 bp2 xp2
