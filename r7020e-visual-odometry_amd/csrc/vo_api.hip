@@ -241,8 +241,9 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
         // every stream at the default priority: the forked SIFT streams must not rank below the
         // geometry / copy streams of the pipelined loop body (at the lowest priority the full
         // per-frame path dropped from 7.3 k to 5.4 k stereo frames/s), and the scale-space stream
-        // at the highest priority measured within noise.  No CU masks: partitioning the CUs
-        // between the two streams measured within noise
+        // at the highest priority measured within noise.  No CU masks: with masks that bind
+        // (contiguous CU ranges), every split of the CUs between the two streams was 9-38 %
+        // slower -- both streams are bound per CU and need the whole chip
         e = hipStreamCreateWithFlags(&c->sub[k], hipStreamNonBlocking);
         if (e != hipSuccess) return bail("stream", e);
         if ((e = hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
