@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <utility>
 #include <type_traits>
+#include <mutex>
 
 namespace vo {
 
@@ -1527,9 +1528,10 @@ __global__ __launch_bounds__(64, 5) void k_desc(const Pyramid* __restrict__ py, 
 #pragma unroll
             for (int u = 0; u < U; ++u) {                // phase 1b: all gradient loads in flight together
                 const float* gp = gim + off[u];           // (every listed sample is valid)
-                // the row neighbours x-1 .. x+1 as one 12-B load: 3 loads per sample instead of 4
-                typedef float f3_t __attribute__((ext_vector_type(3)));
-                const f3_t h = *reinterpret_cast<const f3_t*>(gp - 1);
+                // the row neighbours x-1 .. x+1 as one 12-B load (3 loads per sample instead of 4);
+                // through a 3-float vector type declared with the 4-B alignment the address has
+                typedef float f3u_t __attribute__((ext_vector_type(3), aligned(4)));
+                const f3u_t h = *reinterpret_cast<const f3u_t*>(gp - 1);
                 g4[u][0] = h.z; g4[u][1] = h.x;
                 g4[u][2] = gp[-(ptrdiff_t)P]; g4[u][3] = gp[P];
             }
@@ -1634,6 +1636,21 @@ static Kern make_kern(const Pyramid& py, int level)
     return k;
 }
 
+// hipFuncSetAttribute is a per-device setting: raise a kernel's dynamic-LDS limit to the CU's
+// 160 KB once per (kernel, device), so a second context on another device gets it too
+static void raise_lds_limit(const void* fn)
+{
+    static std::mutex mu;
+    static std::vector<std::pair<const void*, int>> done;
+    int dev = 0;
+    hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lock(mu);
+    for (const auto& d : done)
+        if (d.first == fn && d.second == dev) return;
+    hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    done.push_back({fn, dev});
+}
+
 template <int RAD, int MODE>
 static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t plane, size_t dplane, int pitch, int R, int C,
                           float* g, float* d, const Kern& K, const ImageSrc& isrc, int in_rows, int in_cols, const char* name)
@@ -1676,13 +1693,7 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
     }
     // generic tiled form: kernel radii without a streaming instantiation, planes shorter than
     // one band (tiny images; GPU edge tests), and the non-upsampled / split octave-0 base
-    if (lds > 64 * 1024) {
-        static bool once = false;
-        if (!once) {
-            hipFuncSetAttribute((const void*)k_blur_fused<RAD, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            once = true;
-        }
-    }
+    if (lds > 64 * 1024) raise_lds_limit((const void*)k_blur_fused<RAD, MODE>);
     VO_LAUNCH_NAMED(MODE == 0 ? "k_blur_fused" : "k_blur_base", (k_blur_fused<RAD, MODE>), grid, dim3(256), lds, s, src,
                     plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols);
 }
@@ -1728,11 +1739,7 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
         const OctGeom& g = py.oct[o];
         const int R = g.rows, C = g.cols;
         if (o == o_small) {
-            static bool attr = false;
-            if (!attr) {
-                hipFuncSetAttribute((const void*)k_small_pyr, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-                attr = true;
-            }
+            raise_lds_limit((const void*)k_small_pyr);
             VO_LAUNCH_NAMED("k_blur_small", k_small_pyr, dim3(n_img), dim3(VO_SMALL_T), small_lds, s, d_py, A, o,
                             small_rtab);
             break;

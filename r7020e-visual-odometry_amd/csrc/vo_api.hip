@@ -450,7 +450,9 @@ static int stage_images(vo_ctx* c, const uint8_t* img, int ld, int col_major, in
         HIPC(c, hipMemcpy2DAsync(dst, cols, img, ld, cols, (size_t)rows * n, hipMemcpyHostToDevice, c->stream));
         return VO_OK;
     }
-    const size_t need = (size_t)ld * cols * n;
+    // exactly the bytes the frames span: the last column of the last frame ends `rows` bytes
+    // into its ld-byte slot (a padded view, ld > rows, must not be read past its end)
+    const size_t need = (size_t)ld * ((size_t)cols * n - 1) + rows;
     if (need > c->cm_cap) {
         HIPC(c, hipStreamSynchronize(c->stream));
         hipFree(c->d_cm);

@@ -81,9 +81,7 @@ struct Pyramid {
 };
 
 #ifndef VO_EXT_BAND
-#ifndef VO_EXT_BAND
 #define VO_EXT_BAND 30            // interior rows per extremum-test wave (a multiple of 3)
-#endif
 #endif
 #define VO_SEG_WORDS 1024
 

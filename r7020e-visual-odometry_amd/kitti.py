@@ -262,8 +262,11 @@ def _pipelined(ctx, batches, dev, on_collect=None) -> list:
         if on_collect is not None:
             on_collect(b0, L, outs)
     for b0, L, R in batches:
-        if isinstance(L, torch.Tensor):                       # device-resident frames (ready at the call)
+        if isinstance(L, torch.Tensor):                       # device-resident frames
             dl, dr = L.contiguous(), R.contiguous()
+            # the frames' producer (and any .contiguous() copy) ran on torch's current stream,
+            # which libvo's non-blocking streams do not wait for
+            torch.cuda.current_stream(dl.device).synchronize()
             L = L.cpu().numpy() if on_collect is not None else None
         else:
             dl = torch.from_numpy(L).pin_memory().to(dev, non_blocking=True)

@@ -239,11 +239,18 @@ class Context:
     def sift(self, img: np.ndarray):
         """A Fortran-ordered image (MATLAB's layout) goes to vo_sift_ex untransposed."""
         img = np.asarray(img, np.uint8)
-        if img.strides[0] == 1 and img.ndim == 2 and img.shape[0] > 1:
+        if img.ndim != 2:
+            raise VOError(VO_ERR_ARG, "sift: a 2-D uint8 image")
+        rows, cols = img.shape
+        # zero-copy only for positive strides the ABI can express (ld >= rows column-major,
+        # ld >= cols row-major); flipped or otherwise strided views are packed first
+        if rows > 1 and img.strides[0] == 1 and img.strides[1] >= rows:
             col_major, ld = 1, img.strides[1]
-        else:
-            img = np.ascontiguousarray(img) if img.strides[1] != 1 else img
+        elif img.strides[1] == 1 and img.strides[0] >= cols:
             col_major, ld = 0, img.strides[0]
+        else:
+            img = np.ascontiguousarray(img)
+            col_major, ld = 0, cols
         cap = self.sift_params.max_keypoints
         kps = np.zeros(cap, KP_DTYPE)
         desc = np.zeros((cap, 128), np.uint8)

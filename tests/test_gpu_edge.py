@@ -133,3 +133,28 @@ def test_column_major_images_equal_row_major(vo, oracle, syn):
     lb = ctx.get_landmarks()
     assert a.tobytes() == b.tobytes() and np.array_equal(la, lb)
     ctx.close()
+
+
+def test_padded_and_flipped_views(vo, oracle, syn):
+    """Strided host views through vo_sift_ex: a padded Fortran view (ld > rows, the staging copy
+    stops at the last pixel rather than ld * cols bytes), a padded row-major view, and flipped
+    views (negative strides are packed on the host) -- all equal the oracle on the same pixels."""
+    L, _ = syn.stereo_pair(syn.SEED_BASE + 89)
+    ctx = vo.Context(375, 1242, 1)
+    rk, rd = oracle.sift(L)
+    big = np.zeros((390, 1242), np.uint8, order="F")
+    big[10:385] = L
+    view = big[10:385]                                    # Fortran, ld = 390 > rows = 375
+    assert view.strides == (1, 390)
+    k, d = ctx.sift(view)
+    assert np.array_equal(k, rk) and np.array_equal(d, rd)
+    wide = np.zeros((375, 1300), np.uint8)
+    wide[:, :1242] = L
+    k, d = ctx.sift(wide[:, :1242])                       # row-major, ld = 1300
+    assert np.array_equal(k, rk) and np.array_equal(d, rd)
+    fk, fd = oracle.sift(np.ascontiguousarray(L[::-1]))
+    k, d = ctx.sift(L[::-1])                              # negative row stride
+    assert np.array_equal(k, fk) and np.array_equal(d, fd)
+    k, d = ctx.sift(np.asfortranarray(L)[::-1])           # Fortran order, negative row stride
+    assert np.array_equal(k, fk) and np.array_equal(d, fd)
+    ctx.close()
