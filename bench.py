@@ -136,7 +136,7 @@ def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks)
     ok = steps["status"][1:] == 0
     # the reference's own run (VO.m on MATLAB, the real KITTI-00 images): its lagged x-z error
     # curve digitised from reference 4500/error.png (tests/golden/digitize_ref_error.py)
-    ref_curve = np.loadtxt(ROOT / "tests" / "golden" / "kitti" / "ref_error_digitized.csv", delimiter=",")
+    ref_curve = np.loadtxt(ROOT / "data" / "kitti" / "ref_error_digitized.csv", delimiter=",")
     return {"metric": "stereo frames/sec, full per-frame path over the KITTI-00 trajectory (BASELINE configs[2]; configs[3] at 8 GPUs)",
             "value": n / el, "unit": "stereo frames/s", "frames": n, "frames_per_rank": e - s, "batch": SB,
             "partition": f"block + one-frame halo over {world} rank(s); all-gather of per-frame records and landmark rows",
@@ -154,7 +154,7 @@ def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks)
                              "mean": float(ref_curve[:, 1].mean()), "max": float(ref_curve[:, 1].max()),
                              "final": float(ref_curve[-1, 1]),
                              "source": "VO.m on MATLAB over the real KITTI-00 images, digitised from reference "
-                                       "4500/error.png (tests/golden/kitti/ref_error_digitized.csv); different input "
+                                       "4500/error.png (data/kitti/ref_error_digitized.csv); different input "
                                        "images than this run, so context rather than parity"}},
             "render_s": render_s,
             "data": "synthetic street world rendered along reference kitti/poses/00.txt with kitti/00/calib.txt P0/P1 "

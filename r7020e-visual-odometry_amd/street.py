@@ -39,8 +39,8 @@ from pathlib import Path
 import numpy as np
 
 ROOT = Path(__file__).resolve().parent.parent
-KITTI00_POSES = ROOT / "tests" / "golden" / "kitti" / "poses_00.txt"
-KITTI00_CALIB = ROOT / "tests" / "golden" / "kitti" / "calib_00.txt"
+KITTI00_POSES = ROOT / "data" / "kitti" / "poses_00.txt"
+KITTI00_CALIB = ROOT / "data" / "kitti" / "calib_00.txt"
 KITTI_ROWS, KITTI_COLS = 376, 1241
 CAM_HEIGHT = 1.65
 

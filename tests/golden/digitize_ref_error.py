@@ -1,6 +1,6 @@
 """Digitise the reference's published KITTI-00 accuracy curve (reference 4500/error.png: the
 lagged x-z error of PlotOnMap.m:8-20 for VO.m's MATLAB run on the real KITTI-00 images) into
-tests/golden/kitti/ref_error_digitized.csv (time [s], error [m]) -- a data fixture, the only
+data/kitti/ref_error_digitized.csv (time [s], error [m]) -- a data fixture, the only
 numeric output of the reference's own run that the repository holds.
 
 Plot geometry (read from the PNG): axes box x 64..741 px = 0..500 s, y 562..28 px = 0..45 m;
@@ -33,6 +33,6 @@ def digitize(path):
 if __name__ == "__main__":
     src = sys.argv[1] if len(sys.argv) > 1 else "/root/reference/4500/error.png"
     d = digitize(src)
-    dst = Path(__file__).resolve().parent / "kitti" / "ref_error_digitized.csv"
+    dst = Path(__file__).resolve().parent.parent.parent / "data" / "kitti" / "ref_error_digitized.csv"
     np.savetxt(dst, d, fmt="%.3f", delimiter=",", header="time_s,lagged_xz_error_m (digitised from reference 4500/error.png)")
     print(f"{len(d)} samples, t {d[0, 0]:.1f}..{d[-1, 0]:.1f} s, error mean {d[:, 1].mean():.2f} max {d[:, 1].max():.2f} final {d[-1, 1]:.2f} m")

@@ -1,12 +1,14 @@
 """KITTI I/O, trajectory output, accuracy evaluation and map persistence (SURVEY §8(f) rows
-1-3).  Fixtures under tests/golden/kitti/ are the reference's own data files (calib.txt and
-the first 60 lines of poses/00.txt and times.txt of KITTI-00)."""
+1-3).  The reference's own KITTI-00 data files: calib.txt, poses/00.txt, times.txt and the
+digitised error curve in data/kitti/ (the package reads them), the first 60 lines of
+poses/00.txt and times.txt under tests/golden/kitti/."""
 from pathlib import Path
 
 import numpy as np
 import pytest
 
 GOLD = Path(__file__).resolve().parent / "golden" / "kitti"
+DATA = Path(__file__).resolve().parent.parent / "data" / "kitti"
 
 
 @pytest.fixture(scope="module")
@@ -17,7 +19,7 @@ def kitti():
 
 
 def test_calib_matches_vo_m_constants(kitti, syn):
-    cal = kitti.read_calib(GOLD / "calib_00.txt")
+    cal = kitti.read_calib(DATA / "calib_00.txt")
     assert set(cal) >= {"P0", "P1", "P2", "P3"}
     # VO.m:35-38 intrinsics: fu = fv = 718.856, principal point 607.1928, 185.2157
     assert cal["P0"][0, 0] == 718.856 and cal["P0"][1, 1] == 718.856
@@ -81,7 +83,7 @@ def write_kitti_layout(root: Path, L: np.ndarray, R: np.ndarray, seq: str = "00"
         (d / name).mkdir(parents=True, exist_ok=True)
         for i, im in enumerate(imgs):
             Image.fromarray(im).save(d / name / f"{i:06d}.png")
-    (d / "calib.txt").write_text((GOLD / "calib_00.txt").read_text())
+    (d / "calib.txt").write_text((DATA / "calib_00.txt").read_text())
     (d / "times.txt").write_text("\n".join(f"{0.1 * i:.6e}" for i in range(len(L))) + "\n")
 
 
@@ -120,8 +122,8 @@ def test_reference_error_curve_fixture():
     images), digitised into a fixture by tests/golden/digitize_ref_error.py: 0..470.5 s (KITTI-00's
     times.txt span), peak ~40.8 m near t = 460 s, final ~34.6 m."""
     from pathlib import Path
-    d = np.loadtxt(Path(__file__).parent / "golden" / "kitti" / "ref_error_digitized.csv", delimiter=",")
-    t = np.loadtxt(Path(__file__).parent / "golden" / "kitti" / "times_00.txt")
+    d = np.loadtxt(DATA / "ref_error_digitized.csv", delimiter=",")
+    t = np.loadtxt(DATA / "times_00.txt")
     assert len(d) > 500 and np.all(np.diff(d[:, 0]) > 0)
     assert abs(d[-1, 0] - t[-1]) < 1.0
     assert 40.0 < d[:, 1].max() < 41.5 and 450 < d[np.argmax(d[:, 1]), 0] < 470

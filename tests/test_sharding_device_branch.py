@@ -1,0 +1,102 @@
+"""The nccl (RCCL) branch of the sharding gathers, on the CPU with a spy in place of
+torch.distributed: with device=<dev> every tensor handed to all_gather is built on that device
+(RCCL only takes device tensors), records and landmark rows come back in frame order from a
+3-rank world, and the results are read back through .cpu().  The spy's device is the CPU (no
+GPU here); what is checked is that the helpers place every collective buffer on the device they
+are given, never on a default one (bench.py passes cuda:LOCAL_RANK under nccl)."""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from r7020e_visual_odometry_amd import sharding
+
+
+class SpyDist(types.SimpleNamespace):
+    """world-size-W all_gather: rank r's contribution is produced by make(r, template)."""
+
+    def __init__(self, world, rank, make):
+        super().__init__()
+        self.world, self.rank, self.make, self.calls = world, rank, make, []
+
+    def get_world_size(self, group=None):
+        return self.world
+
+    def all_gather(self, parts, t, group=None):
+        self.calls.append((t.device, t.dtype, tuple(t.shape)))
+        assert len(parts) == self.world
+        for r in range(self.world):
+            assert parts[r].device == t.device and parts[r].shape == t.shape
+            parts[r].copy_(t if r == self.rank else self.make(r, t))
+
+
+@pytest.fixture
+def spy(monkeypatch):
+    def install(world, rank, make):
+        d = SpyDist(world, rank, make)
+        monkeypatch.setattr(torch.distributed, "get_world_size", d.get_world_size)
+        monkeypatch.setattr(torch.distributed, "all_gather", d.all_gather)
+        return d
+    return install
+
+
+@pytest.mark.parametrize("device", [torch.device("cpu"), "cpu"])
+def test_gather_frames_device_tensors(spy, device):
+    n, W, world = 10, 23, 3
+    full = np.arange(n * W, dtype=np.float64).reshape(n, W) * 0.5
+
+    def make(r, t):
+        s, e = sharding.shard_range(n, world, r)
+        out = torch.zeros_like(t)
+        out[: e - s] = torch.from_numpy(full[s:e])
+        return out
+    d = spy(world, 1, make)
+    s, e = sharding.shard_range(n, world, 1)
+    got = sharding.gather_frames(full[s:e], n, device=device)
+    assert np.array_equal(got, full)
+    assert d.calls and all(c[0] == torch.device(device) and c[1] == torch.float64 for c in d.calls)
+
+
+def test_gather_landmark_rows_device_tensors(spy):
+    world = 3
+    rows = {r: (np.random.default_rng(r).normal(size=(5 + 3 * r, 3)).astype(np.float32),
+                np.random.default_rng(10 + r).random(5 + 3 * r) < 0.7) for r in range(world)}
+
+    def make(r, t):
+        if t.dtype == torch.int64:                                  # the row counts
+            return torch.tensor([len(rows[r][1])], dtype=torch.int64, device=t.device)
+        out = torch.zeros_like(t)
+        X, k = rows[r]
+        out[: len(k), :3] = torch.from_numpy(X)
+        out[: len(k), 3] = torch.from_numpy(k.astype(np.float32))
+        return out
+    dev = torch.device("cpu")
+    d = spy(world, 2, make)
+    X, keep = sharding.gather_landmark_rows(*rows[2], device=dev)
+    assert np.array_equal(X, np.concatenate([rows[r][0] for r in range(world)]))
+    assert np.array_equal(keep, np.concatenate([rows[r][1] for r in range(world)]))
+    assert [c[1] for c in d.calls] == [torch.int64, torch.float32]
+    assert all(c[0] == dev for c in d.calls)
+
+
+def test_gather_steps_frame_order(spy):
+    from r7020e_visual_odometry_amd import vo
+    n, world = 7, 2
+    recs = np.zeros(n, vo.STEP_DTYPE)
+    recs["status"] = [0, 0, -4, 0, 0, 0, -3]
+    recs["n_tracked"] = np.arange(n) * 10
+    recs["rel_pose"] = np.eye(4) + np.arange(n)[:, None, None] * 0.01
+
+    def make(r, t):
+        s, e = sharding.shard_range(n, world, r)
+        rec = np.concatenate([recs["rel_pose"][s:e].reshape(-1, 16)] +
+                             [recs[k][s:e].astype(np.float64).reshape(-1, 1) for k in sharding.STEP_FIELDS], 1)
+        out = torch.zeros_like(t)
+        out[: e - s] = torch.from_numpy(rec)
+        return out
+    spy(world, 0, make)
+    s, e = sharding.shard_range(n, world, 0)
+    steps = sharding.gather_steps(recs[s:e], n, device=torch.device("cpu"))
+    assert np.array_equal(steps["rel_pose"], recs["rel_pose"])
+    assert np.array_equal(steps["status"], recs["status"]) and np.array_equal(steps["n_tracked"], recs["n_tracked"])
