@@ -39,6 +39,7 @@ import numpy as np  # noqa: E402
 
 ROWS, COLS = 375, 1242
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+F64_VECTOR_PEAK_TF = 78.6     # MI355X spec FP64 vector (the guide lists FP32 vector 157.3 TF; FP64 is half)
 I8_MFMA_PEAK_TOPS = 5000.0     # MI355X_MICROARCH.md "Matrix cores": I8 = 2x the dense BF16 ~2.5 PF per clock
 # per-launch HBM bytes of each kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes on this
 # workload (tools/pmc_passes.sh + tools/pmc_traffic.py; FETCH_SIZE doubled on gfx950)
@@ -130,8 +131,31 @@ def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks)
     el = time.perf_counter() - t0
     barrier()
     el = max_over_ranks(el)
+    # per-kernel HIP-event durations of the full path over the block's first PB batches (a
+    # separate profiling pass: vo_step_collect synchronises every stream while profiling, so
+    # these are the kernels' own durations without the pipeline's overlap), ms per SB frames
+    PB = max(1, min(args.profile_steps * 3, (e - h) // SB))
+    ctx.reset()
+    ctx.set_landmark_frame(True)
+    ctx.set_frame_index(h)
+    ctx.set_profiling(True)
+    pouts = np.concatenate(kitti._pipelined(ctx, kitti.device_batches(dL, dR, SB, h, h + PB * SB), torch.device("cuda", local)))
+    fkt = ctx.kernel_times()
+    ctx.set_profiling(False)
     ctx.close()
     del dL, dR
+    fk_ms = {k: round(v[0] / PB, 4) for k, v in sorted(fkt.items(), key=lambda kv: -kv[1][0])}
+    geom = ("k_compose", "k_gather_tri", "k_msac_hyp", "k_msac_score", "k_msac_select", "k_stereo_pos", "k_lm_filter",
+            "k_lm_tri", "k_tri_list")
+    # k_msac_score: every hypothesis slot scores every tracked point -- R X + t (18), two
+    # divisions, K (6), residual and square (5), MSAC sum (1): 32 f64 FLOP per (slot, point)
+    sc_ms = fkt.get("k_msac_score", (0.0, 1))[0]
+    sc_flop = 32.0 * 2048 * float(np.maximum(pouts["n_tracked"], 0).sum())
+    msac = {"kernel": "k_msac_score", "bound": "f64 VALU", "unit": "TFLOP/s (f64)", "flop_per_slot_point": 32,
+            "slots": 2048, "frames": int(len(pouts)), "flop": sc_flop, "ms": sc_ms,
+            "achieved": sc_flop / (sc_ms * 1e-3) / 1e12 if sc_ms > 0 else None, "peak": F64_VECTOR_PEAK_TF,
+            "frac": sc_flop / (sc_ms * 1e-3) / 1e12 / F64_VECTOR_PEAK_TF if sc_ms > 0 else None,
+            "peak_source": "MI355X spec FP64 vector 78.6 TFLOP/s (half the guide's 157.3 TF FP32 vector rate)"}
     err = kitti.lagged_xz_error(poses, gt[:n])
     ok = steps["status"][1:] == 0
     # the reference's own run (VO.m on MATLAB, the real KITTI-00 images): its lagged x-z error
@@ -156,6 +180,10 @@ def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks)
                              "source": "VO.m on MATLAB over the real KITTI-00 images, digitised from reference "
                                        "4500/error.png (data/kitti/ref_error_digitized.csv); different input "
                                        "images than this run, so context rather than parity"}},
+            "kernel_ms_per_step": fk_ms,
+            "geometry_ms_per_step": round(sum(v for k, v in fk_ms.items() if k in geom), 4),
+            "kernel_profile": f"HIP events, first {PB} batches of {SB} frames, collect synchronising every stream",
+            "msac_score_roofline": msac,
             "render_s": render_s,
             "data": "synthetic street world rendered along reference kitti/poses/00.txt with kitti/00/calib.txt P0/P1 "
                     "(KITTI-00 images are not available)",

@@ -45,6 +45,8 @@ hipError_t geom_alloc(GeomBuffers& g, int max_frames, int kp_cap, int n_hyp)
     GA(g.lm_X, sizeof(float) * F * K * 3);
     GA(g.lm_keep, F * K);
     GA(g.lm_rows, sizeof(int) * F);
+    GA(g.lm_pX, sizeof(float) * F * K * 3);
+    GA(g.lm_pkeep, F * K);
 #undef GA
     e = hipMemset(g.step_n, 0, sizeof(int) * 4 * F);
     if (e != hipSuccess) return e;
@@ -56,6 +58,7 @@ void geom_free(GeomBuffers& g)
     hipFree(g.lists); hipFree(g.list_n); hipFree(g.step_i); hipFree(g.step_j); hipFree(g.step_n); hipFree(g.world);
     hipFree(g.imgpt); hipFree(g.oldpos); hipFree(g.inliers); hipFree(g.hyp); hipFree(g.fg); hipFree(g.spos);
     hipFree(g.s_n); hipFree(g.lm_new); hipFree(g.lm_M); hipFree(g.lm_X); hipFree(g.lm_keep); hipFree(g.lm_rows);
+    hipFree(g.lm_pX); hipFree(g.lm_pkeep);
     g = GeomBuffers();
 }
 
@@ -803,6 +806,32 @@ void geom_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_trac
     VO_LAUNCH(k_lm_filter, dim3(B), dim3(1024), 0, s, g.spos, g.s_n, g.oldpos, g.list_n + 3, 4, K, g.lm_keep, g.lm_new,
               g.lm_M, g.lm_rows);
     VO_LAUNCH(k_lm_tri, dim3(16, B), dim3(64), 0, s, g.spos, g.lm_new, g.lm_M, K, cal, g.lm_X, g.lm_keep, g.lm_rows);
+}
+
+// block f: its offset is the sum of the earlier frames' row counts (B <= 128), then a plain copy
+__global__ __launch_bounds__(256) void k_lm_pack(const float* __restrict__ lm_X, const uint8_t* __restrict__ lm_keep,
+                                                 const int* __restrict__ lm_rows, int kp_cap, float* __restrict__ pX,
+                                                 uint8_t* __restrict__ pkeep)
+{
+    const int f = blockIdx.x, tid = threadIdx.x;
+    __shared__ int off;
+    if (tid < 64) {
+        int v = 0;
+        for (int g2 = tid; g2 < f; g2 += 64) v += min(lm_rows[g2], kp_cap);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+        if (tid == 0) off = v;
+    }
+    __syncthreads();
+    const int n = min(lm_rows[f], kp_cap);
+    const float* X = lm_X + (size_t)f * kp_cap * 3;
+    for (int e = tid; e < 3 * n; e += 256) pX[(size_t)off * 3 + e] = X[e];
+    for (int e = tid; e < n; e += 256) pkeep[off + e] = lm_keep[(size_t)f * kp_cap + e];
+}
+
+void lm_pack_launch(GeomBuffers& g, int B, hipStream_t s)
+{
+    VO_LAUNCH(k_lm_pack, dim3(B), dim3(256), 0, s, g.lm_X, g.lm_keep, g.lm_rows, g.kp_cap, g.lm_pX, g.lm_pkeep);
 }
 
 void triangulate_launch(const float* pos, int n, const vo_calib& c, double* X, hipStream_t s)

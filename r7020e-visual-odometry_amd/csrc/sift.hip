@@ -349,6 +349,7 @@ __device__ inline int xcd_remap(int bid, int n)
 
 #define BS_P 4            // prefetch depth (rows); 6 for the octave-0 base measured the same
 
+
 // Scale-space kernels raise their wave priority.  The feature stream's kernels (k_desc,
 // k_orient) are VALU-bound and run beside the scale space of the next batch; a SIMD arbitrates
 // VALU issue by priority, then age, so a freshly dispatched blur wave next to older descriptor
@@ -815,15 +816,16 @@ __device__ __forceinline__ float vo_wave_shl1_or(float old, float x)   // lane i
 
 template <int L>
 __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ py, const float* __restrict__ arena,
-                                                   unsigned long long* __restrict__ mask, float thr, int n_img)
+                                                   unsigned long long* __restrict__ mask, float thr, int n_img, int u_first)
 {
     vo_ss_prio();
     constexpr int NG = L + 3, ND = L + 2, W = 3;      // Gaussian levels, DoG levels, row window
     const int lane = threadIdx.x;
     const int u_all = xcd_remap(blockIdx.x, gridDim.x);
-    const int nu = py->n_units;
+    // units [u_first, n_units) of every image (octaves below u_first's are tested by k_octave)
+    const int nu = py->n_units - u_first;
     const int img = u_all / nu;
-    int u = u_all - img * nu;
+    int u = u_first + u_all - img * nu;
     int o = 0;
     while (o + 1 < py->n_oct && py->ebase[o + 1] <= u) ++o;
     o = __builtin_amdgcn_readfirstlane(o);
@@ -1638,7 +1640,7 @@ static Kern make_kern(const Pyramid& py, int level)
 
 // hipFuncSetAttribute is a per-device setting: raise a kernel's dynamic-LDS limit to the CU's
 // 160 KB once per (kernel, device), so a second context on another device gets it too
-static void raise_lds_limit(const void* fn)
+void raise_lds_limit(const void* fn)
 {
     static std::mutex mu;
     static std::vector<std::pair<const void*, int>> done;
@@ -1713,6 +1715,24 @@ static void launch_blur(dim3 grid, hipStream_t s, const float* src, size_t plane
     }
 }
 
+static float ext_threshold(const Pyramid& py, const vo_sift_params& p)
+{
+    return (float)floor(0.5 * p.contrast_threshold / py.L * 255.0);
+}
+
+// octaves [0, n) whose levels 1..L+2, extremum test and next base k_octave computes in one pass
+// (octave.hip): a prefix of the octaves, below the LDS-sized ones.  Experimental and OFF unless the
+// environment sets VO_FUSED_OCTAVE=1: bit-exact, but measured 2.4x slower than the per-level
+// kernels on MI355X -- read at every enqueue so one process can test both paths.
+static int fused_octaves(const Pyramid& py)
+{
+    const char* e = getenv("VO_FUSED_OCTAVE");
+    if (!e || e[0] != '1') return 0;
+    int n = 0;
+    while (n < py.n_oct && octave_fused_ok(py, n)) ++n;
+    return n;
+}
+
 void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img, const vo_sift_params& p,
                           hipStream_t s, const Pyramid* d_py)
 {
@@ -1735,6 +1755,15 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
         if (!fits || lds > 160 * 1024) break;
         o_small = o; small_rtab = rt; small_lds = lds;
     }
+    const int n_fused = std::min(fused_octaves(py), o_small);
+    if (n_fused > 0) {
+        // k_octave ORs its extremum words into the mask (strips share the words at their
+        // boundaries): clear the fused octaves' words of every image first
+        const size_t w0 = (size_t)py.wbase[0], w1 = (size_t)py.wbase[n_fused * L];
+        hipMemset2DAsync(b.mask + w0, sizeof(unsigned long long) * py.n_words, 0, sizeof(unsigned long long) * (w1 - w0),
+                         n_img, s);
+    }
+    const float thr = ext_threshold(py, p);
     for (int o = 0; o < py.n_oct; ++o) {
         const OctGeom& g = py.oct[o];
         const int R = g.rows, C = g.cols;
@@ -1764,10 +1793,14 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
                 launch_blur<0>(gf, s, b.tmp, g.plane, py.istride, g.pitch, R, C, A + g.g_off[0], nullptr, K0, src, 0, 0,
                                "k_blur_base");
             }
-        } else {
+        } else if (o - 1 >= n_fused) {                 // (a fused octave wrote this base itself)
             const OctGeom& pg = py.oct[o - 1];
             VO_LAUNCH(k_down, dim3((C + 255) / 256, R, n_img), dim3(256), 0, s, A + pg.g_off[L], py.istride, pg.pitch,
                       A + g.g_off[0], py.istride, g.pitch, C);
+        }
+        if (o < n_fused) {
+            octave_fused_launch(py, d_py, b, o, n_img, thr, s);
+            continue;
         }
         for (int i = 1; i < L + 3; ++i) {
             Kern K = make_kern(py, i);
@@ -1791,15 +1824,16 @@ static void sift_enqueue_extrema(const Pyramid& py, SiftBuffers& b, int n_img, c
 {
     const int L = py.L;
     float* A = b.arena;
-    const float thr = (float)floor(0.5 * p.contrast_threshold / L * 255.0);
-    if (py.n_units > 0) {
-        const dim3 ge(py.n_units * n_img);
+    const float thr = ext_threshold(py, p);
+    const int u_first = py.ebase[fused_octaves(py)];
+    if (py.n_units > u_first) {
+        const dim3 ge((py.n_units - u_first) * n_img);
         switch (L) {
-        case 1: VO_LAUNCH(k_ext_stream<1>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
-        case 2: VO_LAUNCH(k_ext_stream<2>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
-        case 3: VO_LAUNCH(k_ext_stream<3>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
-        case 4: VO_LAUNCH(k_ext_stream<4>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
-        default: VO_LAUNCH(k_ext_stream<5>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img); break;
+        case 1: VO_LAUNCH(k_ext_stream<1>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first); break;
+        case 2: VO_LAUNCH(k_ext_stream<2>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first); break;
+        case 3: VO_LAUNCH(k_ext_stream<3>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first); break;
+        case 4: VO_LAUNCH(k_ext_stream<4>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first); break;
+        default: VO_LAUNCH(k_ext_stream<5>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first); break;
         }
     }
 }

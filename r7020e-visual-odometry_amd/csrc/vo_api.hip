@@ -109,7 +109,10 @@ struct vo_ctx {
     // n & 1; its geometry runs on `stream` while the next batch's SIFT runs on sub[0..1].
     // Per set: pinned host copies of the per-frame results and the event that ends the
     // batch (geometry, carry into the other set, result copies).
-    struct StepHost { FrameGeom* fg = nullptr; int* nkp = nullptr; int* np = nullptr; int* rows = nullptr; };
+    struct StepHost {
+        FrameGeom* fg = nullptr; int* nkp = nullptr; int* np = nullptr; int* rows = nullptr;
+        float* pX = nullptr; uint8_t* pkeep = nullptr;   // the batch's packed landmark rows (pinned)
+    };
     StepHost sh[2];
     hipEvent_t ev_step[2] = {};
     hipStream_t copy_stream = nullptr;
@@ -198,6 +201,7 @@ static void destroy_buffers(vo_ctx* c)
     geom_free(c->aux.gb);
     for (int k = 0; k < 2; ++k) {
         hipHostFree(c->sh[k].fg); hipHostFree(c->sh[k].nkp); hipHostFree(c->sh[k].np); hipHostFree(c->sh[k].rows);
+        hipHostFree(c->sh[k].pX); hipHostFree(c->sh[k].pkeep);
         c->sh[k] = vo_ctx::StepHost();
     }
     geom_free(c->gb);
@@ -333,6 +337,8 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
         if ((e = hipHostMalloc((void**)&H.nkp, sizeof(int) * 2 * max_batch, 0)) != hipSuccess) return bail("pinned", e);
         if ((e = hipHostMalloc((void**)&H.np, sizeof(int) * max_batch, 0)) != hipSuccess) return bail("pinned", e);
         if ((e = hipHostMalloc((void**)&H.rows, sizeof(int) * max_batch, 0)) != hipSuccess) return bail("pinned", e);
+        if ((e = hipHostMalloc((void**)&H.pX, sizeof(float) * 3 * max_batch * kp_cap, 0)) != hipSuccess) return bail("pinned", e);
+        if ((e = hipHostMalloc((void**)&H.pkeep, (size_t)max_batch * kp_cap, 0)) != hipSuccess) return bail("pinned", e);
     }
     return c;
 }
@@ -798,6 +804,7 @@ static int submit_batch(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B
     HIPC(c, hipMemcpyAsync(H.nkp, S.sb->n_kp, sizeof(int) * 2 * B, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(H.np, S.pair_n, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(H.rows, S.gb->lm_rows, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
+    lm_pack_launch(*S.gb, B, c->stream);
     if ((rc = enqueue_carry(c, set, B - 1, set ^ 1))) return rc;
     HIPC(c, hipEventRecord(c->ev_step[set], c->stream));
     hipError_t e = hipGetLastError();
@@ -824,18 +831,18 @@ static int collect_batch(vo_ctx* c, vo_step_out* outs, int capacity, int* n_out)
     } else {
         HIPC(c, hipEventSynchronize(c->ev_step[P.set]));
     }
-    std::vector<std::vector<float>> X(B);
-    std::vector<std::vector<uint8_t>> keep(B);
-    for (int f = 0; f < B; ++f) {
-        int r = std::min(H.rows[f], K);
-        X[f].resize((size_t)r * 3);
-        keep[f].resize(r);
-        if (r > 0) {
-            HIPC(c, hipMemcpyAsync(X[f].data(), S.gb->lm_X + (size_t)f * K * 3, sizeof(float) * 3 * r, hipMemcpyDeviceToHost, c->copy_stream));
-            HIPC(c, hipMemcpyAsync(keep[f].data(), S.gb->lm_keep + (size_t)f * K, r, hipMemcpyDeviceToHost, c->copy_stream));
-        }
+    // the batch's landmark rows, packed on the device in frame order (k_lm_pack): one copy each
+    // of X and keep into pinned memory (per-frame copies into pageable vectors cost ~2 x B
+    // staged transfers per batch)
+    size_t total = 0;
+    std::vector<size_t> roff(B + 1, 0);
+    for (int f = 0; f < B; ++f) roff[f + 1] = roff[f] + (size_t)std::min(H.rows[f], K);
+    total = roff[B];
+    if (total > 0) {
+        HIPC(c, hipMemcpyAsync(H.pX, S.gb->lm_pX, sizeof(float) * 3 * total, hipMemcpyDeviceToHost, c->copy_stream));
+        HIPC(c, hipMemcpyAsync(H.pkeep, S.gb->lm_pkeep, total, hipMemcpyDeviceToHost, c->copy_stream));
+        HIPC(c, hipStreamSynchronize(c->copy_stream));
     }
-    HIPC(c, hipStreamSynchronize(c->copy_stream));
     c->pending.pop_front();
     c->last_step_set = P.set;
     c->last_step_B = B;
@@ -853,16 +860,18 @@ static int collect_batch(vo_ctx* c, vo_step_out* outs, int capacity, int* n_out)
                 memcpy(o.rel_pose, H.fg[f].T, sizeof(H.fg[f].T));
                 mat4_mul(c->pose, H.fg[f].T, c->pose);
             }
-            const int r = (int)keep[f].size();
+            const int r = (int)(roff[f + 1] - roff[f]);
+            const float* Xf = H.pX + roff[f] * 3;
+            const uint8_t* kf = H.pkeep + roff[f];
             o.n_landmarks = r;
             if (c->lm_camera) {
-                c->lm_X.insert(c->lm_X.end(), X[f].begin(), X[f].end());
-                c->lm_keep.insert(c->lm_keep.end(), keep[f].begin(), keep[f].end());
+                c->lm_X.insert(c->lm_X.end(), Xf, Xf + (size_t)r * 3);
+                c->lm_keep.insert(c->lm_keep.end(), kf, kf + r);
             } else {
                 size_t base = c->landmarks.size();
                 c->landmarks.resize(base + (size_t)r * 3, 0.0);
                 for (int m = 0; m < r; ++m)
-                    if (keep[f][m]) lm_world(c->pose, &X[f][(size_t)m * 3], &c->landmarks[base + (size_t)m * 3]);
+                    if (kf[m]) lm_world(c->pose, Xf + (size_t)m * 3, &c->landmarks[base + (size_t)m * 3]);
             }
         }
         memcpy(o.pose, c->pose, sizeof(c->pose));

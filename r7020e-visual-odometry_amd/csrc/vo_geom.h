@@ -50,6 +50,10 @@ struct GeomBuffers {
     float* lm_X = nullptr;       // [max_frames][kp_cap][3] camera-frame points of odd rows
     uint8_t* lm_keep = nullptr;  // [max_frames][kp_cap]
     int* lm_rows = nullptr;      // [max_frames]
+    // the batch's landmark rows packed in frame order (one D2H copy per batch): row r of frame f
+    // at sum_{g<f} min(lm_rows[g], kp_cap) + r
+    float* lm_pX = nullptr;      // [max_frames * kp_cap][3]
+    uint8_t* lm_pkeep = nullptr; // [max_frames * kp_cap]
 };
 
 hipError_t geom_alloc(GeomBuffers& g, int max_frames, int kp_cap, int n_hyp);
@@ -80,6 +84,9 @@ void geom_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_trac
 void track_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_track_jobs, const StepArgs& a,
                    const vo_match_params& mp, hipStream_t s);
 static inline int* track_list(const GeomBuffers& g, int f, int l) { return g.lists + ((size_t)f * TL_COUNT + l) * g.kp_cap; }
+
+// Pack frames [0, B)'s landmark rows contiguously into lm_pX / lm_pkeep.
+void lm_pack_launch(GeomBuffers& g, int B, hipStream_t s);
 
 // Standalone launchers used by the single-call ABI functions (frame slot 0).
 // pos: [n][4] (x1, y1, x2, y2) device floats.

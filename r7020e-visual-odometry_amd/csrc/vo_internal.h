@@ -154,6 +154,27 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
 void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
                            const Pyramid* d_py);
 
+// One octave's levels 1..5 + extremum test + next octave base in one pass (octave.hip).
+struct OctArgs {
+    float* arena;
+    size_t istride;                     // floats per image
+    int R, C, pitch, pad0;
+    size_t goff[6];                     // this octave's G_0..G_5 plane offsets
+    float* nbase;                       // next octave's G_0 plane (image 0), or nullptr
+    int Rn, Cn, pitchn, pad1;
+    unsigned long long* mask;
+    int n_words, wr;                    // words per image, words per mask row of this octave
+    int wb[3];                          // word base of layers 1..3 of this octave
+    float thr;                          // extremum threshold (DoG units)
+    float k[6][16];                     // taps of levels 1..5 (k[i][0..r_i])
+    int n_strips, pad2;
+};
+bool octave_fused_ok(const Pyramid& py, int o);
+void octave_fused_launch(const Pyramid& py, const Pyramid* d_py, const SiftBuffers& b, int o, int n_img, float thr,
+                         hipStream_t s);
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize, 160 KB) once per (kernel, device)
+void raise_lds_limit(const void* fn);
+
 // ---------------------------------------------------------------------------
 // Matching.  A match job compares F1 rows (desc[idx1[i]] for i < *n1) against
 // F2 rows.  idx == nullptr means identity.  Counts are read on device.

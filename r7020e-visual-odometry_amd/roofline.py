@@ -13,6 +13,7 @@ bytes per launch / average launch duration of the dominant kernel.
 from __future__ import annotations
 
 import math
+import os
 
 SMALL_PX = 9216   # csrc/sift.hip VO_SMALL_PX
 
@@ -36,11 +37,31 @@ def pyramid_bytes_per_image(rows: int, cols: int, layers: int = 3) -> int:
     return rows * cols + 4 * (2 * G + 2 * D)
 
 
-def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3) -> dict:
+FUSED_MIN_COLS, FUSED_MIN_ROWS = 256, 64   # csrc/octave.hip octave_fused_ok (default SIFT radii, 3 layers)
+
+
+def fused_octaves(rows: int, cols: int, layers: int = 3, enabled: bool | None = None) -> int:
+    """Octaves [0, n) libvo builds with k_octave (levels 1..L+2, extremum test and the next
+    base in one pass): the leading octaves at least 256 columns wide and 64 rows tall -- only
+    when the experimental path is on (VO_FUSED_OCTAVE=1, as csrc/sift.hip fused_octaves reads)."""
+    if enabled is None:
+        enabled = os.environ.get("VO_FUSED_OCTAVE", "0").startswith("1")
+    if layers != 3 or not enabled:
+        return 0
+    dims = octave_dims(rows, cols)
+    o_small = next((o for o in range(1, len(dims)) if all(r * c <= SMALL_PX for r, c in dims[o:])), len(dims))
+    n = 0
+    while n < min(len(dims), o_small) and dims[n][1] >= FUSED_MIN_COLS and dims[n][0] >= FUSED_MIN_ROWS:
+        n += 1
+    return n
+
+
+def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3, fused: bool | None = None) -> dict:
     """Algorithmic bytes per CALL (all launches of that kernel name in one
     batch of n_img images) and launches per call, per kernel name."""
     dims = octave_dims(rows, cols)
     lv = layers + 2          # blurred levels per octave (1..L+2)
+    n_fused = fused_octaves(rows, cols, layers, fused)
     out = {}
 
     def add(name, nbytes, launches):
@@ -56,9 +77,16 @@ def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3) -> dict:
         if o >= o_small:
             add("k_blur_small", 4 * px * (1 + lv), 1 if o == o_small else 0)  # decimated base in, G_0..G_{L+2} out
             continue
-        if o:
+        if o and o - 1 >= n_fused:
             add("k_down", 8 * px, 1)                                      # 1 of 4 source px in, G0 out
+        if o < n_fused:
+            # k_octave: G_0 in once, G_1..G_{L+2} out once, the next octave's base out (1/4 px)
+            nxt = 4 * dims[o + 1][0] * dims[o + 1][1] * n_img if o + 1 < len(dims) else 0
+            add(f"k_octave_o{o}", 4 * px * (1 + lv) + nxt, 1)
+            continue
         add("k_blur_fused", 8 * px * lv, lv)                              # G_{i-1} in, G_i out
-    # extremum test reads the L+3 Gaussian levels of every octave once (DoG formed on chip)
-    add(f"k_ext_stream<{layers}>", sum(4 * (layers + 3) * r * c for r, c in dims) * n_img, 1)
+    # extremum test reads the L+3 Gaussian levels of every other octave once (DoG formed on chip)
+    ext = sum(4 * (layers + 3) * r * c for o, (r, c) in enumerate(dims) if o >= n_fused) * n_img
+    if ext:
+        add(f"k_ext_stream<{layers}>", ext, 1)
     return out

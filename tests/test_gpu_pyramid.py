@@ -47,3 +47,37 @@ def test_gaussian_levels_bit_exact(vo, oracle, syn, shape):
             assert got.shape == plane.shape, (o, i, got.shape, plane.shape)
             bad = np.argwhere(got.view(np.uint32) != plane.view(np.uint32))
             assert bad.size == 0, f"image {img} octave {o} level {i}: {len(bad)} mismatches, first {bad[:4].tolist()}"
+
+
+@pytest.mark.parametrize("shape", [(375, 1242), (400, 1800), (240, 700)])
+def test_experimental_fused_octave_path_equals_default(vo, oracle, syn, shape, monkeypatch):
+    """The experimental k_octave path (octave.hip, VO_FUSED_OCTAVE=1: levels 1..5, extremum test
+    and next base of each large octave in one launch) gives the same Gaussian planes, keypoints,
+    descriptors and stereo pairs as the default per-level kernels, bit for bit."""
+    import torch
+    rows, cols = shape
+    B = 2
+    L = np.empty((B, rows, cols), np.uint8)
+    R = np.empty((B, rows, cols), np.uint8)
+    for f in range(B):
+        L[f], R[f] = syn.stereo_pair(syn.SEED_BASE + 310 + f, rows, cols)
+    dl, dr = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+    torch.cuda.synchronize()
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("VO_FUSED_OCTAVE", flag)
+        ctx = vo.Context(rows, cols, B)
+        ctx.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), B)
+        planes = [ctx.fetch_gaussian(img, o, i) for img in (0, 3) for o in range(3) for i in range(6)]
+        kps = [ctx.fetch_keypoints(img) for img in range(2 * B)]
+        pairs = [ctx.fetch_stereo_pairs(f) for f in range(B)]
+        outs.append((planes, kps, pairs))
+        ctx.close()
+    (p0, k0, s0), (p1, k1, s1) = outs
+    for a, b in zip(p0, p1):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    for (ka, da), (kb, db) in zip(k0, k1):
+        assert ka.tobytes() == kb.tobytes() and np.array_equal(da, db)
+    for a, b in zip(s0, s1):
+        assert np.array_equal(a, b)
+    assert sum(len(ka) for ka, _ in k0) > 100 and sum(len(a) for a in s0) > 20
