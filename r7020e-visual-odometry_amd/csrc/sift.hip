@@ -27,7 +27,9 @@
 
 namespace vo {
 
-struct Kern { float k[VO_SIFT_MAX_RADIUS + 1]; int r; };
+// Level blur taps; nb (image 0's plane, same per-image stride as the output): the streaming blur of
+// level L also stores the next octave's base, its output decimated by 2 (even rows, even columns)
+struct Kern { float k[VO_SIFT_MAX_RADIUS + 1]; int r; float* nb; int nb_pitch, nb_rows, nb_cols; };
 
 // ---------------------------------------------------------------------------
 // geometry (host)
@@ -441,7 +443,8 @@ __device__ __forceinline__ vo_f4 up4_from_words(uint32_t a0, uint32_t a1, uint32
 template <int RAD, bool EDGE, int TAG, int CPL>
 __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, int pitch, int R, int C,
                                                  float* __restrict__ g_out, const Kern& K,
-                                                 int x0, int y0, int TH, float* rb, const U8Src& u8)
+                                                 int x0, int y0, int TH, float* rb, const U8Src& u8,
+                                                 float* __restrict__ nbo)
 {
     // CPL columns per lane (4: 256-column strips, 16-B accesses; 2: 128-column strips,
     // 8-B accesses, half the ring registers -> more waves for the smaller octaves)
@@ -624,6 +627,16 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                 if ((!XCH || (lane >= RH / CPL && lane < 64 - RH / CPL)) && xl < C && y < R) {
                     if (TAG & 2) *reinterpret_cast<vec_t*>(g_out + off) = g;        // cached store variant
                     else __builtin_nontemporal_store(g, reinterpret_cast<vec_t*>(g_out + off));
+                    // next octave's base (level L): even rows, the lane's even columns (xl is even)
+                    if (nbo && !(y & 1) && (y >> 1) < K.nb_rows) {
+                        float* const q = nbo + (size_t)(y >> 1) * K.nb_pitch + (xl >> 1);
+                        if constexpr (CPL == 4) {
+                            if ((xl >> 1) + 1 < K.nb_cols) *reinterpret_cast<vo_f2*>(q) = vo_f2{g[0], g[2]};
+                            else if ((xl >> 1) < K.nb_cols) q[0] = g[0];
+                        } else {
+                            if ((xl >> 1) < K.nb_cols) q[0] = g[0];
+                        }
+                    }
                 }
             }
             if constexpr (!XCH) __syncthreads();
@@ -672,10 +685,11 @@ __global__ __launch_bounds__(64, (RAD <= 6 || CPL == 2) ? 3 : 2) void k_blur_str
         u8.ld = isrc.ld;
         margin = 16;                                       // 8-B word loads stay inside the source row
     }
+    float* const nbo = K.nb ? K.nb + od : nullptr;
     if (x0 - RH < 0 || (XCH ? x0 - RH + 64 * CPL : x0 + SW + RH) + margin > C)
-        blur_stream_body<RAD, true, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, THb, rb, u8);
+        blur_stream_body<RAD, true, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, THb, rb, u8, nbo);
     else
-        blur_stream_body<RAD, false, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, THb, rb, u8);
+        blur_stream_body<RAD, false, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, THb, rb, u8, nbo);
 }
 
 // next octave base: G0 of octave o = G_L of octave o-1 decimated by 2.  Grid (column blocks of
@@ -714,26 +728,31 @@ __global__ __launch_bounds__(VO_SMALL_T) void k_small_pyr(const Pyramid* __restr
     float* base = sm + 3 * VO_SMALL_PX;               // next octave's G_0 (<= VO_SMALL_PX / 4)
     int* ridx = reinterpret_cast<int*>(base + VO_SMALL_PX / 4);       // reflect-101 tables
     int* cidx = ridx + rtab;                          // rtab >= rows + 2r of every octave here
+    // flat sweeps over the plane, element e = tid + k * VO_SMALL_T; its (y, x) advance by
+    // (dy, dx) = divmod(VO_SMALL_T, C) per step (one division per sweep instead of per element)
+    auto sweep = [&](int R, int C, auto&& f) {
+        const int dy = VO_SMALL_T / C, dx = VO_SMALL_T - dy * C;
+        int y = tid / C, x = tid - y * C;
+        for (int e = tid; e < R * C; e += VO_SMALL_T) {
+            f(e, y, x);
+            x += dx; y += dy;
+            if (x >= C) { x -= C; ++y; }
+        }
+    };
     for (int o = o_first; o < py->n_oct; ++o) {
         const OctGeom& g = py->oct[o];
-        const int R = g.rows, C = g.cols, RC = R * C;
+        const int R = g.rows, C = g.cols;
         float* gplane = arena + img * py->istride;
         // ---- G_0 ----
         if (o == o_first) {
             const OctGeom& pg = py->oct[o - 1];
             const float* sp = arena + pg.g_off[L] + img * py->istride;
-            for (int e = tid; e < RC; e += VO_SMALL_T) {
-                const int y = e / C, x = e - y * C;
-                cur[e] = sp[(size_t)(2 * y) * pg.pitch + 2 * x];
-            }
+            sweep(R, C, [&](int e, int y, int x) { cur[e] = sp[(size_t)(2 * y) * pg.pitch + 2 * x]; });
         } else {
-            for (int e = tid; e < RC; e += VO_SMALL_T) cur[e] = base[e];
+            for (int e = tid; e < R * C; e += VO_SMALL_T) cur[e] = base[e];
         }
         __syncthreads();
-        for (int e = tid; e < RC; e += VO_SMALL_T) {
-            const int y = e / C, x = e - y * C;
-            gplane[g.g_off[0] + (size_t)y * g.pitch + x] = cur[e];
-        }
+        sweep(R, C, [&](int e, int y, int x) { gplane[g.g_off[0] + (size_t)y * g.pitch + x] = cur[e]; });
         // ---- levels 1 .. L+2 ----
         for (int i = 1; i < NL; ++i) {
             const int r = py->krad[i];
@@ -741,28 +760,34 @@ __global__ __launch_bounds__(VO_SMALL_T) void k_small_pyr(const Pyramid* __restr
             for (int t = tid; t < R + 2 * r; t += VO_SMALL_T) ridx[t] = vo_reflect101(t - r, R);
             for (int t = tid; t < C + 2 * r; t += VO_SMALL_T) cidx[t] = vo_reflect101(t - r, C);
             __syncthreads();
-            for (int e = tid; e < RC; e += VO_SMALL_T) {                 // row pass
-                const int y = e / C, x = e - y * C;
+            // row pass; interior columns read their taps directly, border columns through the
+            // reflect-101 table (same operands, same order: identical sums)
+            sweep(R, C, [&](int e, int y, int x) {
                 const float* row = cur + y * C;
                 float acc = kk[0] * row[x];
-                for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], row[cidx[x + r - j]] + row[cidx[x + r + j]], acc);
+                if (x >= r && x + r < C) {
+                    for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], row[x - j] + row[x + j], acc);
+                } else {
+                    for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], row[cidx[x + r - j]] + row[cidx[x + r + j]], acc);
+                }
                 tmp[e] = acc;
-            }
+            });
             __syncthreads();
-            for (int e = tid; e < RC; e += VO_SMALL_T) {                 // column pass
-                const int y = e / C, x = e - y * C;
+            sweep(R, C, [&](int e, int y, int x) {                      // column pass
                 float acc = kk[0] * tmp[e];
-                for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], tmp[ridx[y + r - j] * C + x] + tmp[ridx[y + r + j] * C + x], acc);
+                if (y >= r && y + r < R) {
+                    for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], tmp[e - j * C] + tmp[e + j * C], acc);
+                } else {
+                    for (int j = 1; j <= r; ++j)
+                        acc = fmaf(kk[j], tmp[ridx[y + r - j] * C + x] + tmp[ridx[y + r + j] * C + x], acc);
+                }
                 nxt[e] = acc;
                 gplane[g.g_off[i] + (size_t)y * g.pitch + x] = acc;
-            }
+            });
             __syncthreads();
             if (i == L && o + 1 < py->n_oct) {                           // next octave's base: decimated G_L
                 const int C2 = py->oct[o + 1].cols, R2 = py->oct[o + 1].rows;
-                for (int e = tid; e < R2 * C2; e += VO_SMALL_T) {
-                    const int y = e / C2, x = e - y * C2;
-                    base[e] = nxt[(2 * y) * C + 2 * x];
-                }
+                sweep(R2, C2, [&](int e, int y, int x) { base[e] = nxt[(2 * y) * C + 2 * x]; });
             }
             float* t2 = cur; cur = nxt; nxt = t2;
         }
@@ -1653,8 +1678,9 @@ void raise_lds_limit(const void* fn)
     done.push_back({fn, dev});
 }
 
+// -> true when the streaming kernel ran (it stores K.nb, the next octave's base, if set)
 template <int RAD, int MODE>
-static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t plane, size_t dplane, int pitch, int R, int C,
+static bool launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t plane, size_t dplane, int pitch, int R, int C,
                           float* g, float* d, const Kern& K, const ImageSrc& isrc, int in_rows, int in_cols, const char* name)
 {
     const size_t lds = sizeof(float) * ft_lds_floats(K.r);
@@ -1690,7 +1716,7 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
             else if (cpl == 2) VO_BS_GO(0, 2);
             else VO_BS_GO(0, 4);
 #undef VO_BS_GO
-            return;
+            return true;
         }
     }
     // generic tiled form: kernel radii without a streaming instantiation, planes shorter than
@@ -1698,20 +1724,21 @@ static void launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
     if (lds > 64 * 1024) raise_lds_limit((const void*)k_blur_fused<RAD, MODE>);
     VO_LAUNCH_NAMED(MODE == 0 ? "k_blur_fused" : "k_blur_base", (k_blur_fused<RAD, MODE>), grid, dim3(256), lds, s, src,
                     plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols);
+    return false;
 }
 
 template <int MODE>
-static void launch_blur(dim3 grid, hipStream_t s, const float* src, size_t plane, size_t dplane, int pitch, int R, int C, float* g,
+static bool launch_blur(dim3 grid, hipStream_t s, const float* src, size_t plane, size_t dplane, int pitch, int R, int C, float* g,
                         float* d, const Kern& K, const ImageSrc& isrc, int in_rows, int in_cols,
                         const char* name = MODE == 0 ? "k_blur_fused" : "k_blur_base")
 {
     switch (K.r) {
-    case 5: launch_blur_r<5, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
-    case 6: launch_blur_r<6, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
-    case 8: launch_blur_r<8, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
-    case 10: launch_blur_r<10, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
-    case 13: launch_blur_r<13, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
-    default: launch_blur_r<0, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name); break;
+    case 5: return launch_blur_r<5, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name);
+    case 6: return launch_blur_r<6, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name);
+    case 8: return launch_blur_r<8, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name);
+    case 10: return launch_blur_r<10, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name);
+    case 13: return launch_blur_r<13, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name);
+    default: return launch_blur_r<0, MODE>(grid, s, src, plane, dplane, pitch, R, C, g, d, K, isrc, in_rows, in_cols, name);
     }
 }
 
@@ -1764,6 +1791,7 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
                          n_img, s);
     }
     const float thr = ext_threshold(py, p);
+    bool base_done = false;                            // octave o's base already stored
     for (int o = 0; o < py.n_oct; ++o) {
         const OctGeom& g = py.oct[o];
         const int R = g.rows, C = g.cols;
@@ -1793,19 +1821,30 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
                 launch_blur<0>(gf, s, b.tmp, g.plane, py.istride, g.pitch, R, C, A + g.g_off[0], nullptr, K0, src, 0, 0,
                                "k_blur_base");
             }
-        } else if (o - 1 >= n_fused) {                 // (a fused octave wrote this base itself)
+        } else if (o - 1 >= n_fused && !base_done) {  // (a fused octave / level-L blur wrote it)
             const OctGeom& pg = py.oct[o - 1];
             VO_LAUNCH(k_down, dim3((C + 255) / 256, R, n_img), dim3(256), 0, s, A + pg.g_off[L], py.istride, pg.pitch,
                       A + g.g_off[0], py.istride, g.pitch, C);
         }
+        base_done = false;
         if (o < n_fused) {
             octave_fused_launch(py, d_py, b, o, n_img, thr, s);
             continue;
         }
         for (int i = 1; i < L + 3; ++i) {
             Kern K = make_kern(py, i);
-            launch_blur<0>(gf, s, A + g.g_off[i - 1], py.istride, py.istride, g.pitch, R, C, A + g.g_off[i], nullptr, K, src,
-                           0, 0);
+            // level L stores the next octave's base from its store path (no k_down pass: that
+            // re-read the even rows of G_L whole, 1.5x its algorithmic bytes); k_small_pyr
+            // decimates its own first base
+            const bool emit = i == L && o + 1 < o_small;
+            if (emit) {
+                const OctGeom& ng = py.oct[o + 1];
+                K.nb = A + ng.g_off[0];
+                K.nb_pitch = ng.pitch; K.nb_rows = ng.rows; K.nb_cols = ng.cols;
+            }
+            const bool streamed = launch_blur<0>(gf, s, A + g.g_off[i - 1], py.istride, py.istride, g.pitch, R, C,
+                                                 A + g.g_off[i], nullptr, K, src, 0, 0);
+            if (emit) base_done = streamed;
         }
     }
 }

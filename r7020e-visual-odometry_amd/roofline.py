@@ -77,14 +77,15 @@ def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3, fused: bool 
         if o >= o_small:
             add("k_blur_small", 4 * px * (1 + lv), 1 if o == o_small else 0)  # decimated base in, G_0..G_{L+2} out
             continue
-        if o and o - 1 >= n_fused:
-            add("k_down", 8 * px, 1)                                      # 1 of 4 source px in, G0 out
+        # octave o's base (o >= 1, below o_small) is stored by the level-L blur of octave o - 1
+        # (priced with k_blur_fused below); k_blur_small decimates its own first base
         if o < n_fused:
             # k_octave: G_0 in once, G_1..G_{L+2} out once, the next octave's base out (1/4 px)
             nxt = 4 * dims[o + 1][0] * dims[o + 1][1] * n_img if o + 1 < len(dims) else 0
             add(f"k_octave_o{o}", 4 * px * (1 + lv) + nxt, 1)
             continue
-        add("k_blur_fused", 8 * px * lv, lv)                              # G_{i-1} in, G_i out
+        nb = 4 * dims[o + 1][0] * dims[o + 1][1] * n_img if o + 1 < o_small else 0
+        add("k_blur_fused", 8 * px * lv + nb, lv)                         # G_{i-1} in, G_i out (+ next base)
     # extremum test reads the L+3 Gaussian levels of every other octave once (DoG formed on chip)
     ext = sum(4 * (layers + 3) * r * c for o, (r, c) in enumerate(dims) if o >= n_fused) * n_img
     if ext:

@@ -31,11 +31,14 @@ def test_roofline_model_matches_survey():
     assert abs(P - 2.483e6) / 2.483e6 < 0.01                       # P = 2.483 Mpx
     per_frame = 2 * roofline.pyramid_bytes_per_image(375, 1242)
     assert abs(per_frame - 438e6) / 438e6 < 0.01                    # 438 MB / stereo frame
-    # default path: per-level blurs (k_blur_fused, one launch per level of octaves 0..3), k_down
-    # for octaves 1..3, octaves 4..8 (<= 9216 px per plane) in the single LDS-resident k_blur_small
+    # default path: per-level blurs (k_blur_fused, one launch per level of octaves 0..3; level 3
+    # also stores the next octave's base, so no k_down pass), octaves 4..8 (<= 9216 px per
+    # plane) in the single LDS-resident k_blur_small
     kb = roofline.kernel_bytes(375, 1242, 2, fused=False)
     assert roofline.fused_octaves(375, 1242, enabled=False) == 0
-    assert kb["k_blur_fused"][1] == 4 * 5 and kb["k_down"][1] == 3 and kb["k_blur_small"][1] == 1
+    assert kb["k_blur_fused"][1] == 4 * 5 and "k_down" not in kb and kb["k_blur_small"][1] == 1
+    assert kb["k_blur_fused"][0] == 2 * sum(8 * 5 * r * c + (4 * dims[o + 1][0] * dims[o + 1][1] if o < 3 else 0)
+                                            for o, (r, c) in enumerate(dims[:4]))
     assert kb["k_ext_stream<3>"][0] == 2 * sum(4 * 6 * r * c for r, c in dims)
     # experimental k_octave path (VO_FUSED_OCTAVE=1): octaves 0..3 (>= 256 columns, >= 64 rows)
     # are one launch each (levels, extremum test, next base)
@@ -47,7 +50,7 @@ def test_roofline_model_matches_survey():
     assert kf["k_octave_o0"][0] == 2 * (4 * R * C * 6 + 4 * dims[1][0] * dims[1][1])   # G0 in, G1..5 out, next base
     # other layer counts keep the per-level kernels
     kb5 = roofline.kernel_bytes(375, 1242, 2, layers=4, fused=True)
-    assert kb5["k_blur_fused"][1] == 4 * 6 and kb5["k_down"][1] == 3
+    assert kb5["k_blur_fused"][1] == 4 * 6 and "k_down" not in kb5
 
 
 def test_libvo_host_chain_and_landmark_transform_equal_references(vo, oracle):
