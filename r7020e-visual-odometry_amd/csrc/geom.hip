@@ -18,6 +18,7 @@
 // Float/double expressions mirror oracle/vo_ref.c operation for operation.
 #include "vo_geom.h"
 #include <cstring>
+#include <cstdlib>
 
 namespace vo {
 
@@ -462,14 +463,10 @@ __device__ __forceinline__ int msac_n(const MsacArgs& a, int f)
     return n < 0 ? 0 : (n > a.kp_cap ? a.kp_cap : n);
 }
 
-// one lane per (frame, slot).  grid (ceil(n_hyp/64), B)
-__global__ __launch_bounds__(64) void k_msac_hyp(MsacArgs a)
+// hypothesis slot s of frame f: Philox sample, Grunert P3P, 4th-point disambiguation
+__device__ void msac_hyp_slot(const MsacArgs& a, int f, int s, int n)
 {
-    const int f = blockIdx.y;
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= a.n_hyp) return;
     MsacHyp* h = a.hyp + (size_t)f * a.n_hyp + s;
-    const int n = msac_n(a, f);
     h->valid = 0;
     if (n < 4 || s >= a.max_trials) return;
     const double* img = a.img + (size_t)f * a.kp_cap * 2;
@@ -496,6 +493,39 @@ __global__ __launch_bounds__(64) void k_msac_hyp(MsacArgs a)
     h->valid = 1;
 }
 
+// one lane per (frame, slot).  grid (ceil(n_hyp/64), B)  (eager form: every slot)
+__global__ __launch_bounds__(64) void k_msac_hyp(MsacArgs a)
+{
+    const int f = blockIdx.y;
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.n_hyp) return;
+    msac_hyp_slot(a, f, s, msac_n(a, f));
+}
+
+// MSAC score of one valid slot by one wave: 64 lane-strided partials + the fixed shuffle tree
+__device__ __forceinline__ void msac_score_slot(const MsacArgs& a, int f, int s, int n, int lane)
+{
+    MsacHyp* h = a.hyp + (size_t)f * a.n_hyp + s;
+    const double* img = a.img + (size_t)f * a.kp_cap * 2;
+    const double* world = a.world + (size_t)f * a.kp_cap * 3;
+    double R[9], tt[3];
+    for (int q = 0; q < 9; ++q) R[q] = h->R[q];
+    for (int q = 0; q < 3; ++q) tt[q] = h->t[q];
+    double part = 0.0;
+    int cnt = 0;
+    for (int k = lane; k < n; k += 64) {
+        double e = reproj_err2_dev(R, tt, a.K, world + 3 * k, img + 2 * k);
+        if (e < a.thr) cnt++;
+        part = part + (e < a.thr ? e : a.thr);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        part = part + __shfl_down(part, off);
+        cnt += __shfl_xor(cnt, off);
+    }
+    if (lane == 0) { h->score = part; h->n_in = cnt; }
+}
+
 // one wave per (frame, slot): MSAC score = 64 lane-strided partials + tree
 __global__ __launch_bounds__(256) void k_msac_score(MsacArgs a, int B)
 {
@@ -503,27 +533,8 @@ __global__ __launch_bounds__(256) void k_msac_score(MsacArgs a, int B)
     const long total = (long)B * a.n_hyp;
     for (long t = (long)blockIdx.x * 4 + (threadIdx.x >> 6); t < total; t += (long)gridDim.x * 4) {
         const int f = (int)(t / a.n_hyp), s = (int)(t - (long)f * a.n_hyp);
-        MsacHyp* h = a.hyp + (size_t)f * a.n_hyp + s;
-        if (!h->valid) continue;
-        const int n = msac_n(a, f);
-        const double* img = a.img + (size_t)f * a.kp_cap * 2;
-        const double* world = a.world + (size_t)f * a.kp_cap * 3;
-        double R[9], tt[3];
-        for (int q = 0; q < 9; ++q) R[q] = h->R[q];
-        for (int q = 0; q < 3; ++q) tt[q] = h->t[q];
-        double part = 0.0;
-        int cnt = 0;
-        for (int k = lane; k < n; k += 64) {
-            double e = reproj_err2_dev(R, tt, a.K, world + 3 * k, img + 2 * k);
-            if (e < a.thr) cnt++;
-            part = part + (e < a.thr ? e : a.thr);
-        }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            part = part + __shfl_down(part, off);
-            cnt += __shfl_xor(cnt, off);
-        }
-        if (lane == 0) { h->score = part; h->n_in = cnt; }
+        if (!a.hyp[(size_t)f * a.n_hyp + s].valid) continue;
+        msac_score_slot(a, f, s, msac_n(a, f), lane);
     }
 }
 
@@ -540,6 +551,8 @@ __device__ int msac_trials_needed_dev(int n_in, int n, double conf)
     if (N < 1.0) return 1;
     return (int)N;
 }
+
+__device__ void msac_final(const MsacArgs& a, int f, int n, int best, int status, int lane);
 
 // sequential MSAC replay (adaptive trial count) + final inliers/pose.  block 64 per frame
 __global__ __launch_bounds__(64) void k_msac_select(MsacArgs a)
@@ -574,8 +587,14 @@ __global__ __launch_bounds__(64) void k_msac_select(MsacArgs a)
         g->n_tracked = n;
     }
     __syncthreads();
-    const int best = s_best;
-    if (s_status != VO_OK) {
+    msac_final(a, f, n, s_best, s_status, lane);
+}
+
+// inlier mask + camera pose of the chosen slot (one wave)
+__device__ void msac_final(const MsacArgs& a, int f, int n, int best, int status, int lane)
+{
+    FrameGeom* g = a.fg + f;
+    if (status != VO_OK) {
         if (lane == 0) {
             g->n_inliers = 0;
             for (int q = 0; q < 16; ++q) g->T[q] = (q % 5 == 0) ? 1.0 : 0.0;
@@ -604,6 +623,64 @@ __global__ __launch_bounds__(64) void k_msac_select(MsacArgs a)
         }
         g->T[12] = 0; g->T[13] = 0; g->T[14] = 0; g->T[15] = 1;
     }
+}
+
+// Lazy MSAC: one 1024-thread block per frame walks the slots in chunks of 64 -- generate the
+// chunk's hypotheses (lane per slot), score its valid ones (wave per slot), replay the
+// sequential adaptive-termination loop over the chunk (thread 0, state carried across chunks)
+// -- and stops at the chunk where the replay stops.  At the ~97 % inlier ratios of the KITTI
+// path the replay needs ~3 trials, so one chunk of 64 replaces 2048 eager slots.  Same
+// slots, same per-slot arithmetic, same replay: results identical to the eager kernels.
+#define VO_MSAC_CHUNK 64
+#define VO_MSAC_T 1024            // 16 waves: a chunk's 64 slots scored 4 per wave (one block per frame)
+__global__ __launch_bounds__(VO_MSAC_T) void k_msac(MsacArgs a)
+{
+    __shared__ int s_best, s_status, s_done;
+    const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int n = msac_n(a, f);
+    const int limit = a.max_trials < a.n_hyp ? a.max_trials : a.n_hyp;
+    FrameGeom* g = a.fg + f;
+    // replay state (thread 0)
+    int num_trials = a.max_trials, trials = 0, best_in = 0, best = -1;
+    double best_score = INFINITY;
+    if (tid == 0) s_done = n < 4;
+    __syncthreads();
+    for (int c0 = 0; !s_done && c0 < limit; c0 += VO_MSAC_CHUNK) {
+        const int c1 = min(c0 + VO_MSAC_CHUNK, limit);
+        if (tid < c1 - c0) msac_hyp_slot(a, f, c0 + tid, n);
+        __syncthreads();                                    // the chunk's slots are written
+        for (int s = c0 + wv; s < c1; s += VO_MSAC_T / 64)
+            if (a.hyp[(size_t)f * a.n_hyp + s].valid) msac_score_slot(a, f, s, n, lane);
+        __syncthreads();                                    // ... and scored
+        if (tid == 0) {
+            int s = c0;
+            for (; s < c1 && trials < num_trials; ++s) {
+                const MsacHyp* h = a.hyp + (size_t)f * a.n_hyp + s;
+                if (!h->valid) continue;
+                trials++;
+                if (h->score < best_score) {
+                    best_score = h->score; best = s; best_in = h->n_in;
+                    int need = msac_trials_needed_dev(h->n_in, n, a.conf);
+                    if (need < num_trials) num_trials = need;
+                }
+            }
+            s_done = trials >= num_trials || s >= limit;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        int status = VO_OK;
+        if (n < 4) status = VO_ERR_TOO_FEW_POINTS;
+        else if (best < 0 || best_in < 4) status = VO_ERR_NO_CONSENSUS;
+        s_best = best;
+        s_status = status;
+        g->status = status;
+        g->best = best;
+        g->n_tracked = n;
+    }
+    __syncthreads();
+    if (wv) return;
+    msac_final(a, f, n, s_best, s_status, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -772,6 +849,13 @@ static MsacArgs msac_args(GeomBuffers& g, const double* img, const double* world
 
 static void msac_enqueue(const MsacArgs& a, int B, hipStream_t s)
 {
+    // VO_MSAC_EAGER=1: the eager form (every slot generated and scored, then the replay) --
+    // kept as the cross-check of the lazy kernel (tests/test_gpu_geom.py)
+    const char* e = getenv("VO_MSAC_EAGER");
+    if (!(e && e[0] == '1')) {
+        VO_LAUNCH(k_msac, dim3(B), dim3(VO_MSAC_T), 0, s, a);
+        return;
+    }
     VO_LAUNCH(k_msac_hyp, dim3((a.n_hyp + 63) / 64, B), dim3(64), 0, s, a);
     int blocks = (B * a.n_hyp + 3) / 4;
     if (blocks > 4096) blocks = 4096;
