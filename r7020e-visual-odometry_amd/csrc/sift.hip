@@ -728,31 +728,26 @@ __global__ __launch_bounds__(VO_SMALL_T) void k_small_pyr(const Pyramid* __restr
     float* base = sm + 3 * VO_SMALL_PX;               // next octave's G_0 (<= VO_SMALL_PX / 4)
     int* ridx = reinterpret_cast<int*>(base + VO_SMALL_PX / 4);       // reflect-101 tables
     int* cidx = ridx + rtab;                          // rtab >= rows + 2r of every octave here
-    // flat sweeps over the plane, element e = tid + k * VO_SMALL_T; its (y, x) advance by
-    // (dy, dx) = divmod(VO_SMALL_T, C) per step (one division per sweep instead of per element)
-    auto sweep = [&](int R, int C, auto&& f) {
-        const int dy = VO_SMALL_T / C, dx = VO_SMALL_T - dy * C;
-        int y = tid / C, x = tid - y * C;
-        for (int e = tid; e < R * C; e += VO_SMALL_T) {
-            f(e, y, x);
-            x += dx; y += dy;
-            if (x >= C) { x -= C; ++y; }
-        }
-    };
     for (int o = o_first; o < py->n_oct; ++o) {
         const OctGeom& g = py->oct[o];
-        const int R = g.rows, C = g.cols;
+        const int R = g.rows, C = g.cols, RC = R * C;
         float* gplane = arena + img * py->istride;
         // ---- G_0 ----
         if (o == o_first) {
             const OctGeom& pg = py->oct[o - 1];
             const float* sp = arena + pg.g_off[L] + img * py->istride;
-            sweep(R, C, [&](int e, int y, int x) { cur[e] = sp[(size_t)(2 * y) * pg.pitch + 2 * x]; });
+            for (int e = tid; e < RC; e += VO_SMALL_T) {
+                const int y = e / C, x = e - y * C;
+                cur[e] = sp[(size_t)(2 * y) * pg.pitch + 2 * x];
+            }
         } else {
-            for (int e = tid; e < R * C; e += VO_SMALL_T) cur[e] = base[e];
+            for (int e = tid; e < RC; e += VO_SMALL_T) cur[e] = base[e];
         }
         __syncthreads();
-        sweep(R, C, [&](int e, int y, int x) { gplane[g.g_off[0] + (size_t)y * g.pitch + x] = cur[e]; });
+        for (int e = tid; e < RC; e += VO_SMALL_T) {
+            const int y = e / C, x = e - y * C;
+            gplane[g.g_off[0] + (size_t)y * g.pitch + x] = cur[e];
+        }
         // ---- levels 1 .. L+2 ----
         for (int i = 1; i < NL; ++i) {
             const int r = py->krad[i];
@@ -760,34 +755,28 @@ __global__ __launch_bounds__(VO_SMALL_T) void k_small_pyr(const Pyramid* __restr
             for (int t = tid; t < R + 2 * r; t += VO_SMALL_T) ridx[t] = vo_reflect101(t - r, R);
             for (int t = tid; t < C + 2 * r; t += VO_SMALL_T) cidx[t] = vo_reflect101(t - r, C);
             __syncthreads();
-            // row pass; interior columns read their taps directly, border columns through the
-            // reflect-101 table (same operands, same order: identical sums)
-            sweep(R, C, [&](int e, int y, int x) {
+            for (int e = tid; e < RC; e += VO_SMALL_T) {                 // row pass
+                const int y = e / C, x = e - y * C;
                 const float* row = cur + y * C;
                 float acc = kk[0] * row[x];
-                if (x >= r && x + r < C) {
-                    for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], row[x - j] + row[x + j], acc);
-                } else {
-                    for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], row[cidx[x + r - j]] + row[cidx[x + r + j]], acc);
-                }
+                for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], row[cidx[x + r - j]] + row[cidx[x + r + j]], acc);
                 tmp[e] = acc;
-            });
+            }
             __syncthreads();
-            sweep(R, C, [&](int e, int y, int x) {                      // column pass
+            for (int e = tid; e < RC; e += VO_SMALL_T) {                 // column pass
+                const int y = e / C, x = e - y * C;
                 float acc = kk[0] * tmp[e];
-                if (y >= r && y + r < R) {
-                    for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], tmp[e - j * C] + tmp[e + j * C], acc);
-                } else {
-                    for (int j = 1; j <= r; ++j)
-                        acc = fmaf(kk[j], tmp[ridx[y + r - j] * C + x] + tmp[ridx[y + r + j] * C + x], acc);
-                }
+                for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], tmp[ridx[y + r - j] * C + x] + tmp[ridx[y + r + j] * C + x], acc);
                 nxt[e] = acc;
                 gplane[g.g_off[i] + (size_t)y * g.pitch + x] = acc;
-            });
+            }
             __syncthreads();
             if (i == L && o + 1 < py->n_oct) {                           // next octave's base: decimated G_L
                 const int C2 = py->oct[o + 1].cols, R2 = py->oct[o + 1].rows;
-                sweep(R2, C2, [&](int e, int y, int x) { base[e] = nxt[(2 * y) * C + 2 * x]; });
+                for (int e = tid; e < R2 * C2; e += VO_SMALL_T) {
+                    const int y = e / C2, x = e - y * C2;
+                    base[e] = nxt[(2 * y) * C + 2 * x];
+                }
             }
             float* t2 = cur; cur = nxt; nxt = t2;
         }
