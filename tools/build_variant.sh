@@ -1,14 +1,15 @@
 #!/bin/bash
 # Build libvo with extra compile definitions into tools/variants/<name>/libvo.so (experiments;
 # bench.py / tests pick a variant up with VO_LIBPATH).   bash tools/build_variant.sh <name> -DX=Y ...
-# VO_SRC=<dir> builds from another copy of csrc (e.g. a git revision exported to /tmp).
+# VO_SRC=<dir> builds from another copy of csrc (e.g. a git revision exported to /tmp), VO_INC=<dir>
+# with that revision's include/.
 set -e
 NAME=$1; shift
 D=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$D/tools/variants/$NAME
 mkdir -p $OUT/obj
 cd ${VO_SRC:-$D/r7020e-visual-odometry_amd/csrc}
-FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I$D/include -I. $*"
+FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I${VO_INC:-$D/include} -I. $*"
 for f in sift octave match geom vo_api; do
   X=""; [ $f = match ] && X="-mllvm -amdgpu-mfma-vgpr-form"
   /opt/rocm/bin/hipcc $FL $X -c $f.hip -o $OUT/obj/$f.o &
