@@ -330,6 +330,8 @@ __global__ __launch_bounds__(256) void k_blur_fused(const float* __restrict__ sr
 // k_blur_fused's (row pass, then column pass, same order).
 // ---------------------------------------------------------------------------
 typedef float vo_f2 __attribute__((ext_vector_type(2)));
+typedef int vo_i2 __attribute__((ext_vector_type(2)));
+typedef int vo_i4 __attribute__((ext_vector_type(4)));
 typedef float vo_f4 __attribute__((ext_vector_type(4)));
 
 // compile-time loop: f(std::integral_constant<int, 0>) ... f(<N-1>), so array
@@ -481,6 +483,12 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
     float k[RAD + 1];
 #pragma unroll
     for (int j = 0; j <= RAD; ++j) k[j] = K.k[j];
+    static_assert(P % 2 == 0, "the next-base rows are the even steps of a block");
+    // buffer descriptors (wave-uniform: kernel arguments and block-derived offsets) of this
+    // image's output plane and of the next octave's base plane (size 0 when not stored)
+    const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(g_out, 0, R * pitch * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_nb =
+        __builtin_amdgcn_make_buffer_rsrc(nbo, 0, nbo ? K.nb_rows * K.nb_pitch * 4 : 0, 0x00020000);
 
     vec_t pf[P], ph[P];
     typedef uint32_t u2_t __attribute__((ext_vector_type(2)));
@@ -563,7 +571,7 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                 for (int i = 0; i < CPL * NQ; ++i) w[i] = 0.0f;
                 vec_t vm, vh;
                 fetch(uc, kk, vm, vh);
-                if (kk + P < F + TH) VO_BS_LOAD(kk + P, u);   // no prefetch past the band's last row
+                VO_BS_LOAD(min(kk + P, F + TH - 1), u);   // past the band's end: its last row again (an L2 hit)
                 vo_dpp_window<RAD, CPL>(vm, w);
             } else {
                 float* const row = rb;
@@ -574,7 +582,7 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                     *reinterpret_cast<vec_t*>(hpos >= 0 ? row + hpos : dummy) = vh;
                 }
                 __syncthreads();                          // one-wave block: orders the LDS row only
-                if (kk + P < F + TH) VO_BS_LOAD(kk + P, u);   // no prefetch past the band's last row
+                VO_BS_LOAD(min(kk + P, F + TH - 1), u);   // past the band's end: its last row again (an L2 hit)
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const vec_t t = (TAG & 32) ? (q & 1 ? vh : vm) : *reinterpret_cast<const vec_t*>(row + CPL * lane + CPL * q);
@@ -621,21 +629,36 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                 }
                 // nothing reads a plane's row padding (columns >= C), so lanes past the last
                 // column store nothing (3 % of the octave-0 level writes); XCH: the halo lanes
-                // store nothing either
+                // store nothing either.  Buffer stores whose inactive lanes get an out-of-range
+                // offset (the hardware drops them): every step issues the same VMEM instructions
+                // unconditionally.  (A store -- or a prefetch -- under a branch made the compiler's
+                // waitcnt pass assume it might have been skipped and drain the queue with
+                // vmcnt(0) once per block, so the rows prefetched P steps ahead were waited for
+                // 1-3 steps after issue.)
                 const int y = y0 + kk - F;
-                const size_t off = (size_t)y * pitch + xl;
-                if ((!XCH || (lane >= RH / CPL && lane < 64 - RH / CPL)) && xl < C && y < R) {
-                    if (TAG & 2) *reinterpret_cast<vec_t*>(g_out + off) = g;        // cached store variant
-                    else __builtin_nontemporal_store(g, reinterpret_cast<vec_t*>(g_out + off));
-                    // next octave's base (level L): even rows, the lane's even columns (xl is even)
-                    if (nbo && !(y & 1) && (y >> 1) < K.nb_rows) {
-                        float* const q = nbo + (size_t)(y >> 1) * K.nb_pitch + (xl >> 1);
-                        if constexpr (CPL == 4) {
-                            if ((xl >> 1) + 1 < K.nb_cols) *reinterpret_cast<vo_f2*>(q) = vo_f2{g[0], g[2]};
-                            else if ((xl >> 1) < K.nb_cols) q[0] = g[0];
-                        } else {
-                            if ((xl >> 1) < K.nb_cols) q[0] = g[0];
-                        }
+                const bool act = (!XCH || (lane >= RH / CPL && lane < 64 - RH / CPL)) && xl < C && y < R;
+                constexpr uint32_t OOB = 0x80000000u;
+                const uint32_t vo = act ? (uint32_t)(y * pitch + xl) * 4u : OOB;
+                constexpr int AUX = (TAG & 2) ? 0 : 2;           // 2: non-temporal (TAG & 2: cached store variant)
+                if constexpr (CPL == 4)
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(vo_i4, g), rs_out, vo, 0, AUX);
+                else
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(vo_i2, g), rs_out, vo, 0, AUX);
+                // next octave's base (level L; K.nb unset: a zero-size buffer drops it): even rows
+                // -- the even steps u, since y0, F and kk0 - F are multiples of P -- and the lane's
+                // even columns (xl is even)
+                if constexpr ((u & 1) == 0) {
+                    const int yn = y >> 1, c0 = xl >> 1;
+                    const bool rowok = act && yn < K.nb_rows;
+                    const uint32_t nbase = (uint32_t)(yn * K.nb_pitch + c0) * 4u;
+                    if constexpr (CPL == 4) {
+                        const bool two = rowok && c0 + 1 < K.nb_cols, one = rowok && !two && c0 < K.nb_cols;
+                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(vo_i2, vo_f2{g[0], g[2]}), rs_nb,
+                                                              two ? nbase : OOB, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, g[0]), rs_nb, one ? nbase : OOB, 0, 0);
+                    } else {
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, g[0]), rs_nb,
+                                                              rowok && c0 < K.nb_cols ? nbase : OOB, 0, 0);
                     }
                 }
             }
@@ -830,14 +853,16 @@ __device__ __forceinline__ float vo_wave_shl1_or(float old, float x)   // lane i
 
 template <int L>
 __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ py, const float* __restrict__ arena,
-                                                   unsigned long long* __restrict__ mask, float thr, int n_img, int u_first)
+                                                   unsigned long long* __restrict__ mask, float thr, int n_img, int u_first,
+                                                   int u_last)
 {
     vo_ss_prio();
     constexpr int NG = L + 3, ND = L + 2, W = 3;      // Gaussian levels, DoG levels, row window
     const int lane = threadIdx.x;
     const int u_all = xcd_remap(blockIdx.x, gridDim.x);
-    // units [u_first, n_units) of every image (octaves below u_first's are tested by k_octave)
-    const int nu = py->n_units - u_first;
+    // units [u_first, u_last) of every image (a range of octaves; those below a fused prefix
+    // are tested by k_octave)
+    const int nu = u_last - u_first;
     const int img = u_all / nu;
     int u = u_first + u_all - img * nu;
     int o = 0;
@@ -1749,16 +1774,14 @@ static int fused_octaves(const Pyramid& py)
     return n;
 }
 
-void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img, const vo_sift_params& p,
-                          hipStream_t s, const Pyramid* d_py)
+// First octave from which every remaining octave fits the one-launch LDS path (k_small_pyr),
+// its reflect-table length and dynamic LDS size.
+struct SmallPlan { int o_small, rtab; size_t lds; };
+static SmallPlan small_plan(const Pyramid& py)
 {
-    const int L = py.L;
-    float* A = b.arena;
-    // first octave from which every remaining octave fits the one-launch LDS path
-    int o_small = py.n_oct, small_rtab = 0;
-    size_t small_lds = 0;
+    SmallPlan sp{py.n_oct, 0, 0};
     int maxr = 0;
-    for (int i = 1; i < L + 3; ++i) maxr = std::max(maxr, py.krad[i]);
+    for (int i = 1; i < py.L + 3; ++i) maxr = std::max(maxr, py.krad[i]);
     for (int o = py.n_oct - 1; o >= 1; --o) {
         int rt = 0, ct = 0;
         bool fits = true;
@@ -1769,8 +1792,31 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
         }
         const size_t lds = sizeof(float) * (3 * VO_SMALL_PX + VO_SMALL_PX / 4) + sizeof(int) * (rt + ct);
         if (!fits || lds > 160 * 1024) break;
-        o_small = o; small_rtab = rt; small_lds = lds;
+        sp = SmallPlan{o, rt, lds};
     }
+    return sp;
+}
+
+// The LDS-sized octaves (one k_small_pyr launch).  Enqueued at the head of the feature stages,
+// not at the tail of the scale space: each of its workgroups needs ~120 KB of one CU's LDS, which
+// the scale-space stream only finds once the previous batch's descriptor waves (6.7 KB each, up
+// to 20 per CU) have drained -- at the head of the feature stream they have, by stream order.
+static void sift_enqueue_small(const Pyramid& py, SiftBuffers& b, int n_img, hipStream_t s, const Pyramid* d_py)
+{
+    const SmallPlan sp = small_plan(py);
+    if (sp.o_small >= py.n_oct) return;
+    raise_lds_limit((const void*)k_small_pyr);
+    VO_LAUNCH_NAMED("k_blur_small", k_small_pyr, dim3(n_img), dim3(VO_SMALL_T), sp.lds, s, d_py, b.arena, sp.o_small,
+                    sp.rtab);
+}
+
+void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img, const vo_sift_params& p,
+                          hipStream_t s, const Pyramid* d_py, hipEvent_t ev_o0)
+{
+    const int L = py.L;
+    float* A = b.arena;
+    const SmallPlan sp = small_plan(py);
+    const int o_small = sp.o_small;
     const int n_fused = std::min(fused_octaves(py), o_small);
     if (n_fused > 0) {
         // k_octave ORs its extremum words into the mask (strips share the words at their
@@ -1784,12 +1830,7 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
     for (int o = 0; o < py.n_oct; ++o) {
         const OctGeom& g = py.oct[o];
         const int R = g.rows, C = g.cols;
-        if (o == o_small) {
-            raise_lds_limit((const void*)k_small_pyr);
-            VO_LAUNCH_NAMED("k_blur_small", k_small_pyr, dim3(n_img), dim3(VO_SMALL_T), small_lds, s, d_py, A, o,
-                            small_rtab);
-            break;
-        }
+        if (o == o_small) break;                       // octaves o_small.. : sift_enqueue_small
         dim3 gf((C + FT_W - 1) / FT_W, (R + FT_H - 1) / FT_H, n_img);
         if (o == 0) {
             Kern K0 = make_kern(py, 0);
@@ -1835,6 +1876,7 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
                                                  A + g.g_off[i], nullptr, K, src, 0, 0);
             if (emit) base_done = streamed;
         }
+        if (o == 0 && ev_o0) hipEventRecord(ev_o0, s);           // octave 0 complete: its extremum test may start
     }
 }
 
@@ -1847,29 +1889,35 @@ constexpr int kFeatureGrid = 32768;
 // The extremum test runs at the head of the feature stages, not at the tail of the scale
 // space: the scale-space stream is the pipeline's critical path (7.1 of 7.9 ms per 64-frame
 // step in situ, against 4.7 ms of feature stages), so the test's 1.7 ms balance the streams.
-static void sift_enqueue_extrema(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
-                                 const Pyramid* d_py)
+void sift_enqueue_extrema(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
+                          const Pyramid* d_py, int o_begin, int o_end)
 {
     const int L = py.L;
     float* A = b.arena;
     const float thr = ext_threshold(py, p);
-    const int u_first = py.ebase[fused_octaves(py)];
-    if (py.n_units > u_first) {
-        const dim3 ge((py.n_units - u_first) * n_img);
+    const int u_first = py.ebase[std::max(o_begin, fused_octaves(py))], u_last = py.ebase[o_end];
+    if (u_last > u_first) {
+        const dim3 ge((u_last - u_first) * n_img);
         switch (L) {
-        case 1: VO_LAUNCH(k_ext_stream<1>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first); break;
-        case 2: VO_LAUNCH(k_ext_stream<2>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first); break;
-        case 3: VO_LAUNCH(k_ext_stream<3>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first); break;
-        case 4: VO_LAUNCH(k_ext_stream<4>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first); break;
-        default: VO_LAUNCH(k_ext_stream<5>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first); break;
+        case 1: VO_LAUNCH(k_ext_stream<1>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first, u_last); break;
+        case 2: VO_LAUNCH(k_ext_stream<2>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first, u_last); break;
+        case 3: VO_LAUNCH(k_ext_stream<3>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first, u_last); break;
+        case 4: VO_LAUNCH(k_ext_stream<4>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first, u_last); break;
+        default: VO_LAUNCH(k_ext_stream<5>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first, u_last); break;
         }
     }
+}
+
+void sift_enqueue_pyramid_tail(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
+                               const Pyramid* d_py, int ext_o_begin)
+{
+    sift_enqueue_small(py, b, n_img, s, d_py);
+    sift_enqueue_extrema(py, b, n_img, p, s, d_py, ext_o_begin, py.n_oct);
 }
 
 void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
                            const Pyramid* d_py)
 {
-    sift_enqueue_extrema(py, b, n_img, p, s, d_py);
     float* A = b.arena;
     const dim3 gs(py.n_seg > 0 ? py.n_seg : 1, n_img);
     VO_LAUNCH(k_seg_count, gs, dim3(256), 0, s, b.mask, b.woff, py.n_words, py.n_seg);
@@ -1891,6 +1939,7 @@ void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_
                   hipStream_t s, const Pyramid* d_py)
 {
     sift_enqueue_pyramid(py, b, src, n_img, p, s, d_py);
+    sift_enqueue_pyramid_tail(py, b, n_img, p, s, d_py, 0);
     sift_enqueue_features(py, b, n_img, p, s, d_py);
 }
 

@@ -69,7 +69,7 @@ struct vo_ctx {
     static constexpr int MAX_SUB = 4;
     int n_sub = 1;
     hipStream_t sub[MAX_SUB] = {};                 // sub[0]: scale-space stream, sub[1]: feature stream
-    hipEvent_t ev_fork = nullptr, ev_join[MAX_SUB] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[MAX_SUB] = {}, ev_o0[MAX_SUB] = {};
     // Asynchronous batch pipeline (vo_sift_match_batch_dev): calls alternate between two
     // buffer sets; set 0 is the context's own buffers (sb, mb, stereo jobs, pairs), set 1
     // is `aux`.  A call's scale space waits only for the previous use of its own set, so
@@ -178,7 +178,8 @@ static void destroy_streams(vo_ctx* c)
     for (int k = 0; k < vo_ctx::MAX_SUB; ++k) {
         if (c->sub[k]) hipStreamDestroy(c->sub[k]);
         if (c->ev_join[k]) hipEventDestroy(c->ev_join[k]);
-        c->sub[k] = nullptr; c->ev_join[k] = nullptr;
+        if (c->ev_o0[k]) hipEventDestroy(c->ev_o0[k]);
+        c->sub[k] = nullptr; c->ev_join[k] = nullptr; c->ev_o0[k] = nullptr;
     }
     if (c->ev_fork) hipEventDestroy(c->ev_fork);
     c->ev_fork = nullptr;
@@ -251,6 +252,7 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
         e = hipStreamCreateWithFlags(&c->sub[k], hipStreamNonBlocking);
         if (e != hipSuccess) return bail("stream", e);
         if ((e = hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
+        if ((e = hipEventCreateWithFlags(&c->ev_o0[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
     }
     if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("event", e);
     for (int k = 0; k < 2; ++k) {
@@ -600,16 +602,24 @@ static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uin
         HIPC(c, hipStreamWaitEvent(sp, c->ev_fork, 0));
     }
     HIPC(c, hipStreamWaitEvent(sp, c->ev_done[set], 0));      // set free (its previous features done)
+    // scale space on sp; octave 0's extremum test on st as soon as octave 0 is built (beside the
+    // scale space of octaves 1..), the other octaves' at the scale space's tail -- the split
+    // that balances the two streams
     for (int p = 0; p < parts; ++p) {
         const int f0 = B * p / parts, nf = B * (p + 1) / parts - f0;
         ImageSrc src{d_l + f0 * fs, d_r + f0 * fs, fs, c->cols, 0};
         SiftBuffers v = sift_view(*S.sb, c->py, 2 * f0, 2 * nf);
-        sift_enqueue_pyramid(c->py, v, src, 2 * nf, c->sp, sp, c->d_py);
+        sift_enqueue_pyramid(c->py, v, src, 2 * nf, c->sp, sp, c->d_py, c->ev_o0[p]);
+        sift_enqueue_pyramid_tail(c->py, v, 2 * nf, c->sp, sp, c->d_py, 1);
         HIPC(c, hipEventRecord(c->ev_join[p], sp));
     }
     for (int p = 0; p < parts; ++p) {
         const int f0 = B * p / parts, nf = B * (p + 1) / parts - f0;
         SiftBuffers v = sift_view(*S.sb, c->py, 2 * f0, 2 * nf);
+        // (a synchronous profiled call -- bench.py's isolated pass -- starts it after the whole
+        // scale space, so its per-kernel durations stay undisturbed)
+        HIPC(c, hipStreamWaitEvent(st, c->prof.on && join ? c->ev_join[p] : c->ev_o0[p], 0));
+        sift_enqueue_extrema(c->py, v, 2 * nf, c->sp, st, c->d_py, 0, 1);
         HIPC(c, hipStreamWaitEvent(st, c->ev_join[p], 0));
         sift_enqueue_features(c->py, v, 2 * nf, c->sp, st, c->d_py);
         match_launch(match_view(*S.mb, f0), S.jobs + f0, nf, c->mp, st);

@@ -147,10 +147,18 @@ void sift_free(SiftBuffers& b);
 // d_py is a device copy of py.
 void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img,
                   const vo_sift_params& p, hipStream_t s, const Pyramid* d_py);
-// The two phases of sift_enqueue: the scale space (base, level blurs, octave bases), and the
-// feature stages (extremum masks, compaction, refinement, orientation, descriptors).
+// The phases of sift_enqueue: the scale space of the large octaves (base, level blurs, octave
+// bases; ev_o0, if given, is recorded once octave 0 is complete); its tail (the LDS-sized octaves
+// and the extremum test of octaves [ext_o_begin, n_oct)); the extremum test of an octave range;
+// and the feature stages (mask compaction, refinement, orientation, descriptors).  The batched
+// path runs the extremum test of octave 0 on the feature stream as soon as ev_o0 fires, beside
+// the scale space of octaves 1.., and the rest at the scale space's tail (vo_api.hip).
 void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img,
-                          const vo_sift_params& p, hipStream_t s, const Pyramid* d_py);
+                          const vo_sift_params& p, hipStream_t s, const Pyramid* d_py, hipEvent_t ev_o0 = nullptr);
+void sift_enqueue_pyramid_tail(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
+                               const Pyramid* d_py, int ext_o_begin);
+void sift_enqueue_extrema(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
+                          const Pyramid* d_py, int o_begin, int o_end);
 void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
                            const Pyramid* d_py);
 

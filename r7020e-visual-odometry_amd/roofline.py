@@ -87,7 +87,9 @@ def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3, fused: bool 
         nb = 4 * dims[o + 1][0] * dims[o + 1][1] * n_img if o + 1 < o_small else 0
         add("k_blur_fused", 8 * px * lv + nb, lv)                         # G_{i-1} in, G_i out (+ next base)
     # extremum test reads the L+3 Gaussian levels of every other octave once (DoG formed on chip)
+    # two launches when octave 0 is tested separately (on the feature stream, beside the scale
+    # space of octaves 1..; the rest at the scale space's tail)
     ext = sum(4 * (layers + 3) * r * c for o, (r, c) in enumerate(dims) if o >= n_fused) * n_img
     if ext:
-        add(f"k_ext_stream<{layers}>", ext, 1)
+        add(f"k_ext_stream<{layers}>", ext, 2 if n_fused == 0 and len(dims) > 1 else 1)
     return out
