@@ -38,15 +38,41 @@ __device__ __forceinline__ void top2c_merge(float& b, int& i, float& s, float b2
     s = ns;
 }
 
+// Pointers read from the job table are generic to the compiler, so loads through them became
+// flat loads, which count in both vmcnt and lgkmcnt and can only be waited for with vmcnt(0) /
+// lgkmcnt(0): every LDS wait of the tile loop also waited for the next tile's prefetch.  Every
+// job pointer addresses global memory (hipMalloc), so its loads and stores go through the
+// global address space.
+template <class T>
+__device__ __forceinline__ T gld(const T* p)
+{
+    return *(const __attribute__((address_space(1))) T*)p;
+}
+template <class T>
+__device__ __forceinline__ void gst(T* p, T v)
+{
+    *(__attribute__((address_space(1))) T*)p = v;
+}
+
+__device__ __forceinline__ DescMeta gld_meta(const DescMeta* p)
+{
+    typedef int i2_t __attribute__((ext_vector_type(2)));
+    const i2_t v = gld(reinterpret_cast<const i2_t*>(p));       // {sum, inv_norm bits}
+    DescMeta m;
+    m.sum = v.x;
+    m.inv_norm = __int_as_float(v.y);
+    return m;
+}
+
 __device__ __forceinline__ int job_rows(const int* p, int cap)
 {
-    int n = *p;
+    int n = gld(p);
     return n < 0 ? 0 : (n > cap ? cap : n);
 }
 
 __device__ __forceinline__ v4i load_frag(const uint8_t* row, int off)
 {
-    v4i v = *reinterpret_cast<const v4i*>(row + off);
+    v4i v = gld(reinterpret_cast<const v4i*>(row + off));
     v ^= (v4i){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
     return v;
 }
@@ -114,7 +140,7 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
         {
             const int ia = i0 + l31;
             if (ia < n1) {
-                const int ra = J.idx1 ? J.idx1[ia] : ia;
+                const int ra = J.idx1 ? gld(J.idx1 + ia) : ia;
                 const uint8_t* row = J.d1 + (size_t)ra * VO_DESC_LEN;
 #pragma unroll
                 for (int kk = 0; kk < 4; ++kk) a[kk] = load_frag(row, 32 * kk + 16 * h);
@@ -133,8 +159,8 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
             int sa = 0;
             ina[reg] = 0.0f;
             if (row < n1) {
-                const int ra = J.idx1 ? J.idx1[row] : row;
-                const DescMeta m = J.m1[ra];
+                const int ra = J.idx1 ? gld(J.idx1 + row) : row;
+                const DescMeta m = gld_meta(J.m1 + ra);
                 sa = m.sum; ina[reg] = m.inv_norm;
             }
             rk[reg] = 128 * sa - 2097152;
@@ -145,9 +171,9 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
         DescMeta gm;
         auto gload = [&](int jt) {
             const int jc = min(jt + lr, j1 - 1);
-            const int rb = J.idx2 ? J.idx2[jc] : jc;
-            gv = *reinterpret_cast<const v4i*>(J.d2 + (size_t)rb * VO_DESC_LEN + 16 * lseg);
-            if (lseg == 0) gm = J.m2[rb];
+            const int rb = J.idx2 ? gld(J.idx2 + jc) : jc;
+            gv = gld(reinterpret_cast<const v4i*>(J.d2 + (size_t)rb * VO_DESC_LEN + 16 * lseg));
+            if (lseg == 0) gm = gld_meta(J.m2 + rb);
         };
         // After tiles 1, 2, 4, 8, ... of the chunk every lane's second best of a row is raised
         // to the max over the 32 lanes of the half (the row's wave-wide second best so far).
@@ -309,11 +335,11 @@ __global__ __launch_bounds__(1024) void k_match_compact(const MatchJob* __restri
     for (int r = a; r < e; ++r) {
         const int i = R[r];
         if (i >= 0) {
-            if (base < (uint32_t)J.cap) { J.out_i[base] = r; J.out_j[base] = i; }
+            if (base < (uint32_t)J.cap) { gst(J.out_i + base, r); gst(J.out_j + base, i); }
             base++;
         }
     }
-    if (tid == 0) *J.out_n = (int)(total < (uint32_t)J.cap ? total : (uint32_t)J.cap);
+    if (tid == 0) gst(J.out_n, (int)(total < (uint32_t)J.cap ? total : (uint32_t)J.cap));
 }
 
 // Descriptor metadata for externally supplied descriptors (vo_match on host data).

@@ -490,9 +490,16 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
     const __amdgpu_buffer_rsrc_t rs_nb =
         __builtin_amdgcn_make_buffer_rsrc(nbo, 0, nbo ? K.nb_rows * K.nb_pitch * 4 : 0, 0x00020000);
 
-    vec_t pf[P], ph[P];
+    // Prefetch slots.  The DPP layout keeps two sets and alternates them block by block: block
+    // parity b consumes set b and refills set 1-b, so a slot's old value is dead before its
+    // register is loaded again.  With one set the scheduler hoisted each refill above the last
+    // use of the value it replaces, the allocator gave the refill other registers, and the copy
+    // back at the loop edge waited for the load (vmcnt(1) once per block).  (The LDS-staged
+    // layout consumes a slot before its refill by a barrier and keeps one set.)
+    constexpr int NSET = XCH ? 2 : 1;
+    vec_t pf[NSET * P], ph[NSET * P];
     typedef uint32_t u2_t __attribute__((ext_vector_type(2)));
-    u2_t pw[UP && !EDGE ? P : 1][4];                       // UP: raw words (ya main, yb main, ya halo, yb halo)
+    u2_t pw[UP && !EDGE ? NSET * P : 1][4];                // UP: raw words (ya main, yb main, ya halo, yb halo)
     vo_f2 H[NR][NP];
     // UP: source byte column of the first of the 4 bytes feeding outputs xl.. / hx..
     const int gm = (xl >> 1) - 1, gh = (hx >> 1) - 1;
@@ -504,21 +511,34 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
         return v;
     };
 
+    // input row of step kk, reflected (reflect-101).  DPP layout: one fold by selects -- no loop
+    // in the step's control flow, which otherwise split the step into blocks and cost a vmcnt(0)
+    // per block pair; the launch guarantees R > r + P + 2, so a band reads at most r + E < R - 1
+    // rows beyond either edge.  (The LDS layout keeps the general form: the select form raised
+    // its register count past 256.)
+    auto yref = [&](int kk) {
+        const int p = y0 - RAD - E + kk;
+        if constexpr (XCH) return p < 0 ? -p : (p >= R ? 2 * R - 2 - p : p);
+        else return vo_reflect101(p, R);
+    };
     // loads for step kk into prefetch slot SL: input row y0-r-E+kk (reflected)
 #define VO_BS_LOAD(KK, SL)                                                                        \
     do {                                                                                          \
-        const int yin_ = vo_reflect101(y0 - RAD - E + (KK), R);                                   \
+        const int yin_ = yref(KK);                                                                \
         if constexpr (UP) {                                                                       \
             if constexpr (!EDGE) {                                                                \
                 const int ya_ = yin_ >> 1;                                                        \
                 const int yb_ = (yin_ & 1) ? min(ya_ + 1, u8.rows - 1) : max(ya_ - 1, 0);         \
                 const uint8_t* ra_ = u8.p + (size_t)ya_ * u8.ld;                                  \
                 const uint8_t* rb_ = u8.p + (size_t)yb_ * u8.ld;                                  \
-                pw[SL][0] = *reinterpret_cast<const u2_t*>((uintptr_t)(ra_ + gm) & ~(uintptr_t)3); \
-                pw[SL][1] = *reinterpret_cast<const u2_t*>((uintptr_t)(rb_ + gm) & ~(uintptr_t)3); \
+                /* aligned down by pointer arithmetic, not an integer round trip: the pointer */   \
+                /* keeps its global address space, so these are global (in-order) loads, not */    \
+                /* flat ones, which the compiler can only wait for with vmcnt(0) */                 \
+                pw[SL][0] = *reinterpret_cast<const u2_t*>(ra_ + gm - ((uintptr_t)(ra_ + gm) & 3)); \
+                pw[SL][1] = *reinterpret_cast<const u2_t*>(rb_ + gm - ((uintptr_t)(rb_ + gm) & 3)); \
                 if constexpr (!XCH) {                                                             \
-                    pw[SL][2] = *reinterpret_cast<const u2_t*>((uintptr_t)(ra_ + gh) & ~(uintptr_t)3); \
-                    pw[SL][3] = *reinterpret_cast<const u2_t*>((uintptr_t)(rb_ + gh) & ~(uintptr_t)3); \
+                    pw[SL][2] = *reinterpret_cast<const u2_t*>(ra_ + gh - ((uintptr_t)(ra_ + gh) & 3)); \
+                    pw[SL][3] = *reinterpret_cast<const u2_t*>(rb_ + gh - ((uintptr_t)(rb_ + gh) & 3)); \
                 }                                                                                 \
             }                                                                                     \
         } else {                                                                                  \
@@ -539,7 +559,7 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
         vm = pf[SL];
         if constexpr (!XCH) vh = ph[SL];
         if constexpr (UP) {
-            const int yin = vo_reflect101(y0 - RAD - E + kk, R);
+            const int yin = yref(kk);
             if constexpr (!EDGE) {
                 const int ya = yin >> 1, yb = (yin & 1) ? min(ya + 1, u8.rows - 1) : max(ya - 1, 0);
                 const uintptr_t pb = reinterpret_cast<uintptr_t>(u8.p);   // byte misalignment incl. the image base
@@ -561,28 +581,30 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
     // P steps kk0 .. kk0+P-1: exchange input row kk's window (DPP, or staged through LDS),
     // prefetch row kk+P, horizontal pass into ring slot 2r+u, and (STORE) the vertical pass
     // over ring slots u .. u+2r for output row y0 + kk - F; then the ring shifts down by P.
-    auto block = [&](int kk0, auto store_c) {
+    auto block = [&](int kk0, auto store_c, auto par_c) {
+        constexpr int B = decltype(par_c)::value;           // slot set consumed (NSET = 2: 1 - B refilled)
         vo_static_for<P>([&](auto uc) {
             constexpr int u = decltype(uc)::value;
+            constexpr int SC = B * P + u, SN = ((B + 1) % NSET) * P + u;
             const int kk = kk0 + u;
             float w[CPL * NQ];
             if constexpr (XCH) {
 #pragma unroll
                 for (int i = 0; i < CPL * NQ; ++i) w[i] = 0.0f;
                 vec_t vm, vh;
-                fetch(uc, kk, vm, vh);
-                VO_BS_LOAD(min(kk + P, F + TH - 1), u);   // past the band's end: its last row again (an L2 hit)
+                fetch(std::integral_constant<int, SC>{}, kk, vm, vh);
+                VO_BS_LOAD(min(kk + P, F + TH - 1), SN);  // past the band's end: its last row again (an L2 hit)
                 vo_dpp_window<RAD, CPL>(vm, w);
             } else {
                 float* const row = rb;
                 vec_t vm, vh;
-                fetch(uc, kk, vm, vh);
+                fetch(std::integral_constant<int, SC>{}, kk, vm, vh);
                 if (!(TAG & 32)) {                        // TAG & 32: probe variant without LDS staging
                     *reinterpret_cast<vec_t*>(row + RH + CPL * lane) = vm;
                     *reinterpret_cast<vec_t*>(hpos >= 0 ? row + hpos : dummy) = vh;
                 }
                 __syncthreads();                          // one-wave block: orders the LDS row only
-                VO_BS_LOAD(min(kk + P, F + TH - 1), u);   // past the band's end: its last row again (an L2 hit)
+                VO_BS_LOAD(min(kk + P, F + TH - 1), SN);  // past the band's end: its last row again (an L2 hit)
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const vec_t t = (TAG & 32) ? (q & 1 ? vh : vm) : *reinterpret_cast<const vec_t*>(row + CPL * lane + CPL * q);
@@ -615,17 +637,23 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                     }
                 H[2 * RAD + u][c] = acc;
             }
-            if constexpr (decltype(store_c)::value) {
+            // store_c: 0 ring fill (no output), 1 output, 2 decided per step (kk >= F; the
+            // stores are issued either way, dropped during the fill)
+            constexpr int MODE = decltype(store_c)::value;
+            if constexpr (MODE != 0) {
                 vec_t g;
+                if constexpr (MODE == 2) g = vec_t{};
+                if (MODE == 1 || kk >= F) {
 #pragma unroll
-                for (int c = 0; c < NP; ++c) {
-                    vo_f2 acc = vo_f2{k[0], k[0]} * H[u + RAD][c];
-                    if (!(TAG & 16))                      // TAG & 16: probe variant without the column pass
+                    for (int c = 0; c < NP; ++c) {
+                        vo_f2 acc = vo_f2{k[0], k[0]} * H[u + RAD][c];
+                        if (!(TAG & 16))                  // TAG & 16: probe variant without the column pass
 #pragma unroll
-                        for (int j = 1; j <= RAD; ++j)
-                            acc = __builtin_elementwise_fma(vo_f2{k[j], k[j]}, H[u + RAD - j][c] + H[u + RAD + j][c], acc);
-                    g[2 * c] = acc.x;
-                    g[2 * c + 1] = acc.y;
+                            for (int j = 1; j <= RAD; ++j)
+                                acc = __builtin_elementwise_fma(vo_f2{k[j], k[j]}, H[u + RAD - j][c] + H[u + RAD + j][c], acc);
+                        g[2 * c] = acc.x;
+                        g[2 * c + 1] = acc.y;
+                    }
                 }
                 // nothing reads a plane's row padding (columns >= C), so lanes past the last
                 // column store nothing (3 % of the octave-0 level writes); XCH: the halo lanes
@@ -636,7 +664,8 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                 // vmcnt(0) once per block, so the rows prefetched P steps ahead were waited for
                 // 1-3 steps after issue.)
                 const int y = y0 + kk - F;
-                const bool act = (!XCH || (lane >= RH / CPL && lane < 64 - RH / CPL)) && xl < C && y < R;
+                const bool act = (!XCH || (lane >= RH / CPL && lane < 64 - RH / CPL)) && xl < C && y < R &&
+                                 (MODE == 1 || (kk >= F && kk < F + TH));
                 constexpr uint32_t OOB = 0x80000000u;
                 const uint32_t vo = act ? (uint32_t)(y * pitch + xl) * 4u : OOB;
                 constexpr int AUX = (TAG & 2) ? 0 : 2;           // 2: non-temporal (TAG & 2: cached store variant)
@@ -651,14 +680,13 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                     const int yn = y >> 1, c0 = xl >> 1;
                     const bool rowok = act && yn < K.nb_rows;
                     const uint32_t nbase = (uint32_t)(yn * K.nb_pitch + c0) * 4u;
+                    const float g0 = g[0];
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(g0), rs_nb, rowok && c0 < K.nb_cols ? nbase : OOB,
+                                                          0, 0);
                     if constexpr (CPL == 4) {
-                        const bool two = rowok && c0 + 1 < K.nb_cols, one = rowok && !two && c0 < K.nb_cols;
-                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(vo_i2, vo_f2{g[0], g[2]}), rs_nb,
-                                                              two ? nbase : OOB, 0, 0);
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, g[0]), rs_nb, one ? nbase : OOB, 0, 0);
-                    } else {
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, g[0]), rs_nb,
-                                                              rowok && c0 < K.nb_cols ? nbase : OOB, 0, 0);
+                        const float g2 = g[2];
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(g2), rs_nb,
+                                                              rowok && c0 + 1 < K.nb_cols ? nbase + 4u : OOB, 0, 0);
                     }
                 }
             }
@@ -671,10 +699,23 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
     };
 
     vo_static_for<P>([&](auto uc) { VO_BS_LOAD(decltype(uc)::value, decltype(uc)::value); });
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    if constexpr (NSET == 1) {
 #pragma unroll 1
-    for (int kk0 = 0; kk0 < F; kk0 += P) block(kk0, std::false_type{});          // ring fill
+        for (int kk0 = 0; kk0 < F; kk0 += P) block(kk0, I0{}, I0{});               // ring fill
 #pragma unroll 1
-    for (int kk0 = F; kk0 < F + TH; kk0 += P) block(kk0, std::true_type{});      // TH % P == 0
+        for (int kk0 = F; kk0 < F + TH; kk0 += P) block(kk0, I1{}, I0{});          // TH % P == 0
+    } else {
+        // pairs of blocks (set 0, then set 1) from the ring fill on; a pair's second block past
+        // the band's end only re-reads its last row and stores nothing
+#pragma unroll 1
+        for (int kk0 = 0; kk0 < F + TH; kk0 += 2 * P) {
+            block(kk0, I2{}, I0{});
+            block(kk0 + P, I2{}, I1{});
+        }
+    }
 #undef VO_BS_LOAD
 }
 
@@ -1717,7 +1758,7 @@ static bool launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
         const long rows_total = (long)R * n_strips * grid.z;
         int TH = (int)std::min<long>(kMaxTH, rows_total / kWaveTarget);
         TH = std::max(BS_P, TH / BS_P * BS_P);
-        if (R >= TH) {
+        if (R >= TH && R > RAD + BS_P + 2) {             // (one reflection fold per band edge)
             const int n_bands = (R + TH - 1) / TH;
 #define VO_BS_GO(T, CP)                                                                                        \
     do {                                                                                                       \
