@@ -1486,8 +1486,11 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
 // u32 fixed point (vo_desc_fx_quant) sums are order-free, so the copies are folded after
 // the loop without changing a bit.
 #define DCS 324
+#ifndef VO_DESC_WAVES
+#define VO_DESC_WAVES 5           // waves per SIMD the register budget is sized for (96 VGPRs)
+#endif
 template <int DCOPIES>
-__global__ __launch_bounds__(64, 5) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
+__global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                              const KpInt* __restrict__ kpi, const int* __restrict__ n_kp,
                                              uint8_t* __restrict__ desc, DescMeta* __restrict__ meta, int kp_cap, int n_img)
 {
