@@ -74,6 +74,27 @@ VO_HD float vo_expf(float x)
     return (p * s1) * s2;
 }
 
+/* vo_expf on [-87, 0], for callers whose argument is a bounded non-positive quadratic form (the
+ * SIFT window weights): the clamps never fire there, and p * 2^k is formed by one ldexp instead
+ * of two scale factors.  Both forms are the one correctly rounded value of p * 2^k (the first
+ * scale product is exact), so the result equals vo_expf(x) bit for bit on the whole domain --
+ * checked for every float in [-87, 0] by oracle_spec_check_expf_nonpos (tests/test_spec_math.py). */
+VO_HD float vo_expf_nonpos(float x)
+{
+    float kf = rintf(x * 1.44269504088896341f);
+    float r = x - kf * 0.693145751953125f;
+    r = r - kf * 1.42860682030941723212e-6f;
+    float p = 1.98412698e-4f;
+    p = fmaf(p, r, 1.38888889e-3f);
+    p = fmaf(p, r, 8.33333333e-3f);
+    p = fmaf(p, r, 4.16666667e-2f);
+    p = fmaf(p, r, 1.66666667e-1f);
+    p = fmaf(p, r, 0.5f);
+    p = fmaf(p, r, 1.0f);
+    p = fmaf(p, r, 1.0f);
+    return ldexpf(p, (int)kf);
+}
+
 /* ------------------------------------------------------------------------ */
 /* atan2 in DEGREES, result in [0, 360).  (OpenCV fastAtan2 convention:      */
 /* angle of the vector (x, y), counter-clockwise from +x.)  Accurate to      */

@@ -121,6 +121,8 @@ def lib(cv: bool = False):
         L.oracle_spec_eval.argtypes = [C.c_int, P(C.c_double), P(C.c_double), C.c_int]
         L.oracle_spec_eval.restype = None
         L.oracle_philox.argtypes = [C.c_uint32] * 6 + [P(C.c_uint32)]
+        L.oracle_spec_check_expf_nonpos.argtypes = []
+        L.oracle_spec_check_expf_nonpos.restype = C.c_long
         L.oracle_philox.restype = None
         L.oracle_gauss_radius.argtypes = [C.c_double]
         L.oracle_run_sequence.restype = C.c_long
@@ -295,6 +297,11 @@ def sift_match_pair(left, right, sp=None, mp=None):
 
 
 SPEC_FN = {"expf": 0, "atan2_deg": 1, "sin_deg": 2, "cos_deg": 3, "exp_d": 4, "log_d": 5}
+
+
+def spec_check_expf_nonpos() -> int:
+    """Mismatching floats of vo_expf_nonpos vs vo_expf over every float in [-87, 0]."""
+    return int(lib().oracle_spec_check_expf_nonpos())
 
 
 def spec_eval(fn: str, x) -> np.ndarray:

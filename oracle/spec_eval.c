@@ -33,3 +33,17 @@ int oracle_gauss_radius(double sigma)
     float k[VO_SIFT_MAX_RADIUS + 1];
     return vo_gauss_kernel(sigma, k, VO_SIFT_MAX_RADIUS + 1);
 }
+
+/* number of floats x in [-87, 0] (every bit pattern, -0 included) where the specialised window
+ * exponential differs from vo_expf in any bit */
+long oracle_spec_check_expf_nonpos(void)
+{
+    long bad = 0;
+    const uint32_t lo = vo_f32_as_u32(-0.0f), hi = vo_f32_as_u32(-87.0f);
+    for (uint32_t u = lo; u <= hi; ++u) {
+        const float x = vo_u32_as_f32(u);
+        if (vo_f32_as_u32(vo_expf_nonpos(x)) != vo_f32_as_u32(vo_expf(x))) ++bad;
+    }
+    if (vo_f32_as_u32(vo_expf_nonpos(0.0f)) != vo_f32_as_u32(vo_expf(0.0f))) ++bad;
+    return bad;
+}

@@ -1188,6 +1188,26 @@ __device__ __forceinline__ void flat_find(const int* pre, int n_img, long t, int
     k = (int)(t - pre[lo]);
 }
 
+// sqrtf(x), correctly rounded, for x == +0 or 2^-96 <= x < inf: the compiler's IEEE sqrt less its
+// small-argument scaling and special-class select -- v_sqrt_f32 and the same two one-ulp
+// residual corrections, so the value is sqrtf's.  The gradient magnitudes call it on sums of
+// squares and fall back to sqrtf for the whole wave if any lane has 0 < x < 2^-96.
+__device__ __forceinline__ float vo_sqrtf_big(float x)
+{
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rdn = fmaf(-sdn, s, x), rup = fmaf(-sup, s, x);
+    const float s1 = rdn <= 0.0f ? sdn : s;
+    return rup > 0.0f ? sup : s1;
+}
+__device__ __forceinline__ float vo_grad_mag(float dx, float dy)
+{
+    const float x = dx * dx + dy * dy;
+    float m = vo_sqrtf_big(x);
+    if (__builtin_expect(__ballot(x > 0.0f && x < 0x1p-96f) != 0ull, 0)) m = sqrtf(x);   // wave-uniform
+    return m;
+}
+
 #define DAT(p, P, y, x) ((p)[(size_t)(y) * (P) + (x)])
 
 // 3x3 Cramer solve in double (same expression tree as oracle solve3)
@@ -1360,8 +1380,8 @@ __global__ __launch_bounds__(64) void k_orient(const Pyramid* __restrict__ py, c
 #pragma unroll
             for (int q = 0; q < U; ++q) {
                 const float dx = gx[q], dy = gy[q];
-                float w = vo_expf((float)(ii[q] * ii[q] + jj[q] * jj[q]) * expf_scale);
-                float mag = sqrtf(dx * dx + dy * dy);
+                float w = vo_expf_nonpos((float)(ii[q] * ii[q] + jj[q] * jj[q]) * expf_scale);   // arg in [-21, 0]
+                float mag = vo_grad_mag(dx, dy);
                 float ori = vo_atan2_deg(dy, dx);
                 int bin = vo_round((float)VO_SIFT_ORI_BINS / 360.0f * ori);
                 if (bin >= VO_SIFT_ORI_BINS) bin -= VO_SIFT_ORI_BINS;
@@ -1486,8 +1506,25 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
 // u32 fixed point (vo_desc_fx_quant) sums are order-free, so the copies are folded after
 // the loop without changing a bit.
 #define DCS 324
+// paired layout (VO_DESC_PAIR): (DW+2)^2 cells x DN u64 slots = 288, stride 290 u64 (= 4 mod 64 banks)
+#define DCS2 290
+#ifndef VO_DESC_PAIR
+#define VO_DESC_PAIR 0
+#endif
+#ifndef VO_DESC_COPIES
+#define VO_DESC_COPIES 4
+#endif
 #ifndef VO_DESC_WAVES
 #define VO_DESC_WAVES 5           // waves per SIMD the register budget is sized for (96 VGPRs)
+#endif
+#ifndef VO_DESC_LOOP
+#define VO_DESC_LOOP 1            // 1: block row lookup + pipelined gradient loads; 0: per-lane row walk
+#endif
+#ifndef VO_DESC_U
+#define VO_DESC_U 2               // blocks of 64 samples per batch (VO_DESC_LOOP 1)
+#endif
+#ifndef VO_DESC_ADDR
+#define VO_DESC_ADDR 1            // 1: buffer gradient loads from one 32-bit offset, 24-bit index multiplies
 #endif
 template <int DCOPIES>
 __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
@@ -1495,11 +1532,19 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
                                              uint8_t* __restrict__ desc, DescMeta* __restrict__ meta, int kp_cap, int n_img)
 {
     static_assert(DCS >= DHIST, "copy stride holds a histogram");
+#if VO_DESC_PAIR
+    // bin pairs: slot (cell, o) is a u64 whose low word sums bin o and high word bin o+1 (mod DN)
+    // of that cell, so one 64-bit LDS add carries both orientation neighbours of a sample
+    __shared__ uint64_t hfx2[DCOPIES * DCS2];
+    uint32_t* const hfx = reinterpret_cast<uint32_t*>(hfx2);
+#else
     __shared__ uint32_t hfx[DCOPIES * DCS];
-    // per-row first column (16 bit: |j| <= RMAX) and exclusive sample prefix; a row's length is
-    // rstart[r+1] - rstart[r].  < 8 KB of LDS in all -> 5 one-wave workgroups per SIMD
-    __shared__ int16_t rlo[2 * VO_SIFT_DESCR_RMAX + 2];
-    __shared__ int rstart[2 * VO_SIFT_DESCR_RMAX + 3];
+#endif
+    // One packed entry per window row r: (index of the row's first sample) | (its first column j,
+    // int16) << 16; entry nrows is the sample count, entries nrows+1 .. nrows+8 a 0xFFFF sentinel
+    // start.  Starts fit 16 bits: the window holds <= 2 r^2 + O(r) samples (< 34k at r = RMAX).
+    // 7.3 KB of LDS with the histograms -> 5 one-wave workgroups per SIMD.
+    __shared__ uint32_t rtab[2 * VO_SIFT_DESCR_RMAX + 2 + 8];
     const int lane = threadIdx.x;
     __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
     const long total = flat_setup(n_kp, kp_cap, n_img, fpre);
@@ -1512,7 +1557,11 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
         const OctGeom& g = py->oct[q.o];
         const int rows = g.rows, cols = g.cols, P = g.pitch;
         const float* gim = arena + g.g_off[q.layer] + img * py->istride;
+#if VO_DESC_PAIR
+        for (int b = lane; b < DCOPIES * DCS2; b += 64) hfx2[b] = 0ull;
+#else
         for (int b = lane; b < DCOPIES * DCS; b += 64) hfx[b] = 0u;
+#endif
         float ori = 360.0f - q.angle;
         if (fabsf(ori - 360.0f) < VO_FLT_EPSILON) ori = 0.0f;
         const int px = vo_round(q.xo), pyy = vo_round(q.yo);
@@ -1534,23 +1583,28 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
         // still decides every sample, so the histogram is unchanged (fixed-point sums are
         // order-free) while the wave no longer idles through rejected samples.
         const int nrows = 2 * radius + 1;
+        const float inv_ct = fabsf(cos_t) > 1e-9f ? 1.0f / cos_t : 0.0f, inv_st = fabsf(sin_t) > 1e-9f ? 1.0f / sin_t : 0.0f;
         for (int rr = lane; rr < nrows; rr += 64) {
             const int i = rr - radius, r = pyy + i;
             int jlo = -radius, jhi = radius;
             if (r <= 0 || r >= rows - 1) { jlo = 1; jhi = 0; }
             else {
-                const double ct = cos_t, st = sin_t, fi = (double)i, lim = 0.5 * DW + 0.5 + 1e-3;   // rbin = r_rot + 1.5 in (-1, DW)
-                // |j*ct - i*st| < lim  and  |j*st + i*ct| < lim
-                if (fabs(ct) > 1e-9) {
-                    double a = (fi * st - lim) / ct, b = (fi * st + lim) / ct;
-                    if (a > b) { double t2 = a; a = b; b = t2; }
-                    jlo = max(jlo, (int)floor(a) - 2); jhi = min(jhi, (int)ceil(b) + 2);
-                } else if (fabs(fi * st) >= lim) { jlo = 1; jhi = 0; }
-                if (fabs(st) > 1e-9) {
-                    double a = (-fi * ct - lim) / st, b = (-fi * ct + lim) / st;
-                    if (a > b) { double t2 = a; a = b; b = t2; }
-                    jlo = max(jlo, (int)floor(a) - 2); jhi = min(jhi, (int)ceil(b) + 2);
-                } else if (fabs(fi * ct) >= lim) { jlo = 1; jhi = 0; }
+                // |j*ct - i*st| < lim  and  |j*st + i*ct| < lim  (rbin = r_rot + 1.5 in (-1, DW)); lim is
+                // 1e-3 bin widths wider than the test below and the bounds get one column of margin,
+                // far above the float error of these products (< 1e-4 columns at r <= RMAX)
+                const float fi = (float)i, lim = 0.5f * DW + 0.5f + 1e-3f, cap = (float)(radius + 2);
+                if (fabsf(cos_t) > 1e-9f) {
+                    float a = (fi * sin_t - lim) * inv_ct, b = (fi * sin_t + lim) * inv_ct;
+                    if (a > b) { const float t2 = a; a = b; b = t2; }
+                    a = fminf(fmaxf(a, -cap), cap); b = fminf(fmaxf(b, -cap), cap);
+                    jlo = max(jlo, (int)floorf(a) - 1); jhi = min(jhi, (int)ceilf(b) + 1);
+                } else if (fabsf(fi * sin_t) >= lim) { jlo = 1; jhi = 0; }
+                if (fabsf(sin_t) > 1e-9f) {
+                    float a = (-fi * cos_t - lim) * inv_st, b = (-fi * cos_t + lim) * inv_st;
+                    if (a > b) { const float t2 = a; a = b; b = t2; }
+                    a = fminf(fmaxf(a, -cap), cap); b = fminf(fmaxf(b, -cap), cap);
+                    jlo = max(jlo, (int)floorf(a) - 1); jhi = min(jhi, (int)ceilf(b) + 1);
+                } else if (fabsf(fi * cos_t) >= lim) { jlo = 1; jhi = 0; }
                 jlo = max(jlo, 1 - px); jhi = min(jhi, cols - 2 - px);
                 // trim the superset to the exact set: the float test below is monotone
                 // in j on each side (rotations of a row are monotone float sequences),
@@ -1564,100 +1618,225 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
                 while (jlo <= jhi && !inside(jlo)) ++jlo;
                 while (jhi >= jlo && !inside(jhi)) --jhi;
             }
-            rlo[rr] = (int16_t)jlo;
-            rstart[rr + 1] = jhi >= jlo ? jhi - jlo + 1 : 0;       // row length, prefixed below
+            // row length for now (prefixed below), first column in the high half
+            rtab[rr] = (uint32_t)(jhi >= jlo ? jhi - jlo + 1 : 0) | ((uint32_t)(uint16_t)(int16_t)jlo << 16);
         }
         __syncthreads();
-        {   // wave-parallel exclusive prefix over the rows (<= 2*RMAX+1): lane owns a chunk of rows.
-            // All lengths are read (rstart[r+1]) before any start is written (rstart[r]): one
-            // wave, LDS operations in program order.
+        {   // wave-parallel exclusive prefix over the rows (<= 2*RMAX+1): lane owns a chunk of rows
             constexpr int PER_MAX = (2 * VO_SIFT_DESCR_RMAX + 1 + 63) / 64;
             const int per = (nrows + 63) >> 6, r0w = lane * per;
-            int len[PER_MAX];
+            uint32_t ent[PER_MAX];
             int sum = 0;
 #pragma unroll
             for (int q = 0; q < PER_MAX; ++q) {
-                len[q] = (q < per && r0w + q < nrows) ? rstart[r0w + q + 1] : 0;
-                sum += len[q];
+                ent[q] = (q < per && r0w + q < nrows) ? rtab[r0w + q] : 0u;
+                sum += (int)(ent[q] & 0xFFFFu);
             }
             int inc = sum;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(inc, o); if (lane >= o) inc += y; }
-            __syncthreads();
             int acc = inc - sum;
 #pragma unroll
-            for (int q = 0; q < PER_MAX; ++q) if (q < per && r0w + q < nrows) { rstart[r0w + q] = acc; acc += len[q]; }
-            if (lane == 63) rstart[nrows] = inc;
+            for (int q = 0; q < PER_MAX; ++q)
+                if (q < per && r0w + q < nrows) { rtab[r0w + q] = (uint32_t)acc | (ent[q] & 0xFFFF0000u); acc += (int)(ent[q] & 0xFFFFu); }
+            if (lane == 63) rtab[nrows] = (uint32_t)inc;
+            if (lane < 8) rtab[nrows + 1 + lane] = 0xFFFFu;
         }
         __syncthreads();
-        const int nsamp = rstart[nrows];
+#if VO_DESC_DIAG_NOLOOP
+        const int nsamp = 0 * (int)rtab[nrows];   // timing diagnostic only: per-keypoint work without samples
+#else
+        const int nsamp = (int)rtab[nrows];
+#endif
+#if VO_DESC_PAIR
+        uint64_t* hc2 = hfx2 + (lane & (DCOPIES - 1)) * DCS2;
+#else
         uint32_t* hc = hfx + (lane & (DCOPIES - 1)) * DCS;
-        int lo = 0;                                      // current row; s only grows, so advance
-        constexpr int U = 4;                             // samples per lane per iteration: 16 loads in flight
-        for (int s0 = lane; s0 < nsamp; s0 += 64 * U) {
-            float crot[U], rrot[U], gdx[U], gdy[U];
-            bool ok[U];
-            uint32_t off[U];
+#endif
+#if VO_DESC_DIAG_NOATOMIC
+        uint32_t diag = 0;
+#endif
+        // one sample: weights, bins, fixed-point LDS atomics
+        auto accum = [&](float c_rot, float r_rot, float dx, float dy) {
+            float rbin = r_rot + (float)(DW / 2) - 0.5f;
+            float cbin = c_rot + (float)(DW / 2) - 0.5f;
+#if VO_DESC_DIAG_NOMATH
+            // timing diagnostic only (not bit-exact): exp, atan2 and sqrt replaced by cheap terms
+            float w = 1.0f + (c_rot * c_rot + r_rot * r_rot) * exp_scale;
+            float ang = fminf(fabsf(dy) * 57.0f + fabsf(dx), 359.0f);
+            float mag = ((fabsf(dx) + fabsf(dy)) * w) * VO_DESC_FX_SCALE;
+#else
+            float w = vo_expf_nonpos((c_rot * c_rot + r_rot * r_rot) * exp_scale);   // listed samples: arg in (-1.6, 0]
+            float ang = vo_atan2_deg(dy, dx);
+            float mag = (vo_grad_mag(dx, dy) * w) * VO_DESC_FX_SCALE;
+#endif
+            float obin = (ang - ori) * bins_per_deg;
+            // floors kept in float ((float)(int)floorf(v) == floorf(v) here); the cell index is an
+            // exact small-integer float expression, one conversion; obin in [-8, 8] so the circular
+            // wrap of o0 is a mask (DN = 8)
+            const float fr0 = floorf(rbin), fc0 = floorf(cbin), fo0 = floorf(obin);
+            rbin -= fr0; cbin -= fc0; obin -= fo0;
+            const int o0 = (int)fo0 & (DN - 1);
+            const int cell = (int)((fr0 + 1.0f) * (float)(DW + 2) + (fc0 + 1.0f));   // in [0, (DW+2)^2)
+            float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+            float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+            float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+            float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+            float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+            float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+            float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+#if VO_DESC_PAIR
+            uint64_t* h = hc2 + cell * DN + o0;
+            auto pk = [](float lo, float hi) {
+                return (unsigned long long)vo_desc_fx_quant(lo) | ((unsigned long long)vo_desc_fx_quant(hi) << 32);
+            };
+            atomicAdd((unsigned long long*)h, pk(v_rco000, v_rco001));
+            atomicAdd((unsigned long long*)(h + DN), pk(v_rco010, v_rco011));
+            atomicAdd((unsigned long long*)(h + (DW + 2) * DN), pk(v_rco100, v_rco101));
+            atomicAdd((unsigned long long*)(h + (DW + 3) * DN), pk(v_rco110, v_rco111));
+#elif VO_DESC_DIAG_NOATOMIC
+            // timing diagnostic only (not bit-exact): the sample's 8 contributions summed in place
+            uint32_t* h = hc + cell * DBS + o0;
+            diag += vo_desc_fx_quant(v_rco000) + vo_desc_fx_quant(v_rco001) + vo_desc_fx_quant(v_rco010) +
+                    vo_desc_fx_quant(v_rco011) + vo_desc_fx_quant(v_rco100) + vo_desc_fx_quant(v_rco101) +
+                    vo_desc_fx_quant(v_rco110) + vo_desc_fx_quant(v_rco111) + (uint32_t)(size_t)h;
+#else
+            uint32_t* h = hc + (int)((float)cell * (float)DBS) + o0;     // exact: < 2^24
+            atomicAdd(h, vo_desc_fx_quant(v_rco000));
+            atomicAdd(h + 1, vo_desc_fx_quant(v_rco001));
+            atomicAdd(h + DBS, vo_desc_fx_quant(v_rco010));
+            atomicAdd(h + DBS + 1, vo_desc_fx_quant(v_rco011));
+            atomicAdd(h + (DW + 2) * DBS, vo_desc_fx_quant(v_rco100));
+            atomicAdd(h + (DW + 2) * DBS + 1, vo_desc_fx_quant(v_rco101));
+            atomicAdd(h + (DW + 3) * DBS, vo_desc_fx_quant(v_rco110));
+            atomicAdd(h + (DW + 3) * DBS + 1, vo_desc_fx_quant(v_rco111));
+#endif
+        };
+        // the gradient neighbours of a listed sample (every listed sample is interior): x+1, x-1 as
+        // one 12-B load (through a 3-float type declared with the 4-B alignment the address has),
+        // y-1, y+1
+        typedef float f3u_t __attribute__((ext_vector_type(3), aligned(4)));
+#if VO_DESC_ADDR
+        // buffer loads with one 32-bit lane offset: the resource starts at the sample's row y-1
+        // column x-1 for offset 0 (gim - P - 1), so row y-1 is +4 B, row y (x-1..x+1) +4P B and
+        // row y+1 +8P + 4 B -- no 64-bit address arithmetic per sample; the row offset is a
+        // 24-bit multiply (|i| <= RMAX, P < 2^23)
+        const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)(gim - P - 1), 0, 0x7FFFFFF0, 0x00020000);
+        const int c_off = pyy * P + px;                  // wave-uniform
+#endif
+        auto grad_loads = [&](int i, int j, float* g4) {
+#if VO_DESC_DIAG_NOLOAD
+            // timing diagnostic only (not bit-exact): gradients synthesised, no loads
+            g4[0] = (float)(i * 3 + j); g4[1] = (float)(j * 5 - i); g4[2] = (float)(i ^ j); g4[3] = (float)(i - 2 * j);
+#elif VO_DESC_ADDR
+            const int vo = 4 * (c_off + __mul24(i, P) + j);
+            typedef int i3_t __attribute__((ext_vector_type(3)));
+            const i3_t h = __builtin_amdgcn_raw_buffer_load_b96(grs, vo, 4 * P, 0);
+            g4[0] = __int_as_float(h.z); g4[1] = __int_as_float(h.x);
+            g4[2] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 0, 0));
+            g4[3] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 8 * P, 0));
+#else
+            const float* gp = gim + (uint32_t)((pyy + i) * P + px + j);   // 32-bit offset from the uniform base
+            const f3u_t h = *reinterpret_cast<const f3u_t*>(gp - 1);
+            g4[0] = h.z; g4[1] = h.x;
+            g4[2] = gp[-(ptrdiff_t)P]; g4[3] = gp[P];
+#endif
+        };
+#if VO_DESC_LOOP == 0
+        {   // per-lane walk over the row table
+            int lo = 0;                                      // current row; s only grows, so advance
+            constexpr int U = 4;                             // samples per lane per iteration: 16 loads in flight
+            for (int s0 = lane; s0 < nsamp; s0 += 64 * U) {
+                int ii[U], jj[U];
+                bool ok[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {                // phase 1a: rows (LDS walk) and offsets of all U samples
-                const int s = s0 + 64 * u;
-                ok[u] = s < nsamp;
-                const int sc = ok[u] ? s : nsamp - 1;
-                while (rstart[lo + 1] <= sc) ++lo;
-                const int i = lo - radius, j = rlo[lo] + (sc - rstart[lo]);
-                crot[u] = (float)j * cos_t - (float)i * sin_t;
-                rrot[u] = (float)j * sin_t + (float)i * cos_t;
-                off[u] = (uint32_t)((pyy + i) * P + px + j);   // 32-bit offset from the uniform base
-            }
-            float g4[U][4];
+                for (int u = 0; u < U; ++u) {
+                    const int s = s0 + 64 * u;
+                    ok[u] = s < nsamp;
+                    const int sc = ok[u] ? s : nsamp - 1;
+                    while ((int)(rtab[lo + 1] & 0xFFFFu) <= sc) ++lo;
+                    const uint32_t e = rtab[lo];
+                    ii[u] = lo - radius; jj[u] = ((int)e >> 16) + (sc - (int)(e & 0xFFFFu));
+                }
+                float g4[U][4];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {                // phase 1b: all gradient loads in flight together
-                const float* gp = gim + off[u];           // (every listed sample is valid)
-                // the row neighbours x-1 .. x+1 as one 12-B load (3 loads per sample instead of 4);
-                // through a 3-float vector type declared with the 4-B alignment the address has
-                typedef float f3u_t __attribute__((ext_vector_type(3), aligned(4)));
-                const f3u_t h = *reinterpret_cast<const f3u_t*>(gp - 1);
-                g4[u][0] = h.z; g4[u][1] = h.x;
-                g4[u][2] = gp[-(ptrdiff_t)P]; g4[u][3] = gp[P];
-            }
+                for (int u = 0; u < U; ++u) grad_loads(ii[u], jj[u], g4[u]);
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                gdx[u] = g4[u][0] - g4[u][1];
-                gdy[u] = g4[u][2] - g4[u][3];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {                // phase 2: weights, bins, fixed-point LDS atomics
-                if (ok[u]) {
-                const float c_rot = crot[u], r_rot = rrot[u], dx = gdx[u], dy = gdy[u];
-                float rbin = r_rot + (float)(DW / 2) - 0.5f;
-                float cbin = c_rot + (float)(DW / 2) - 0.5f;
-                float w = vo_expf((c_rot * c_rot + r_rot * r_rot) * exp_scale);
-                float ang = vo_atan2_deg(dy, dx);
-                float mag = (sqrtf(dx * dx + dy * dy) * w) * VO_DESC_FX_SCALE;
-                float obin = (ang - ori) * bins_per_deg;
-                int r0 = vo_floor(rbin), c0 = vo_floor(cbin), o0 = vo_floor(obin);
-                rbin -= (float)r0; cbin -= (float)c0; obin -= (float)o0;
-                if (o0 < 0) o0 += DN;
-                if (o0 >= DN) o0 -= DN;
-                float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-                float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
-                float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-                float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
-                float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
-                float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
-                float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-                uint32_t* h = hc + ((r0 + 1) * (DW + 2) + c0 + 1) * DBS + o0;
-                atomicAdd(h, vo_desc_fx_quant(v_rco000));
-                atomicAdd(h + 1, vo_desc_fx_quant(v_rco001));
-                atomicAdd(h + DBS, vo_desc_fx_quant(v_rco010));
-                atomicAdd(h + DBS + 1, vo_desc_fx_quant(v_rco011));
-                atomicAdd(h + (DW + 2) * DBS, vo_desc_fx_quant(v_rco100));
-                atomicAdd(h + (DW + 2) * DBS + 1, vo_desc_fx_quant(v_rco101));
-                atomicAdd(h + (DW + 3) * DBS, vo_desc_fx_quant(v_rco110));
-                atomicAdd(h + (DW + 3) * DBS + 1, vo_desc_fx_quant(v_rco111));
+                for (int u = 0; u < U; ++u) {
+                    if (ok[u]) {
+                        const float fi = (float)ii[u], fj = (float)jj[u];
+                        accum(fj * cos_t - fi * sin_t, fj * sin_t + fi * cos_t, g4[u][0] - g4[u][1], g4[u][2] - g4[u][3]);
+                    }
                 }
             }
         }
+#else
+        {   // Block lookup: the 64 samples bs .. bs+63 of a block start in row rb (wave-uniform) and
+            // span a few rows; every lane reads the same K+2 table entries (LDS broadcast, one round
+            // trip) and selects its row by comparing its sample index with the row starts -- no
+            // per-lane walk, no dependent LDS chain.  Rows past rb+K (short rows at a rotated
+            // window's corners, rows of zero length above the image) take another round.
+            // The gradient loads of the next U blocks are issued before the current U blocks are
+            // accumulated (two slot sets, a pair of batches per loop iteration; the loads of a
+            // batch past the window are clamped to its last sample, so every iteration issues
+            // the same loads and the wait counts stay exact).
+            constexpr int U = VO_DESC_U, K = 4;
+            int rb = 0;                                      // wave-uniform row of the next block's first sample
+            auto locate = [&](int bs, int& i_o, int& j_o) {
+                const int sc = min(bs + lane, nsamp - 1), last = min(bs + 63, nsamp - 1);
+                uint32_t sel = rtab[rb];
+                int row = rb;
+                for (;;) {
+                    const uint32_t* tb = rtab + rb;
+                    uint32_t e[K + 2];
+#pragma unroll
+                    for (int k = 1; k <= K + 1; ++k) e[k] = tb[k];
+#pragma unroll
+                    for (int k = 1; k <= K; ++k) {
+                        const bool c = (int)(e[k] & 0xFFFFu) <= sc;
+                        sel = c ? e[k] : sel;
+                        row += c ? 1 : 0;
+                    }
+                    if ((int)(e[K + 1] & 0xFFFFu) > last) break;   // uniform: every lane's row found
+                    rb += K;
+                }
+                i_o = row - radius;
+                j_o = ((int)sel >> 16) + (sc - (int)(sel & 0xFFFFu));
+                rb = __builtin_amdgcn_readlane(row, 63);
+            };
+            struct Slot { float g[4]; int i, j; };
+            auto issue = [&](int sb, Slot (&S)[U]) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) locate(sb + 64 * u, S[u].i, S[u].j);
+#pragma unroll
+                for (int u = 0; u < U; ++u) grad_loads(S[u].i, S[u].j, S[u].g);
+            };
+            auto consume = [&](int sb, const Slot (&S)[U]) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (sb + 64 * u + lane < nsamp) {
+                        const float fi = (float)S[u].i, fj = (float)S[u].j;
+                        accum(fj * cos_t - fi * sin_t, fj * sin_t + fi * cos_t, S[u].g[0] - S[u].g[1], S[u].g[2] - S[u].g[3]);
+                    }
+                }
+            };
+            if (nsamp > 0) {
+                Slot A[U], B[U];
+                int sb = 0;
+                issue(0, A);
+                for (;;) {
+                    issue(sb + 64 * U, B);
+                    consume(sb, A);
+                    sb += 64 * U;
+                    if (sb >= nsamp) break;
+                    issue(sb + 64 * U, A);
+                    consume(sb, B);
+                    sb += 64 * U;
+                    if (sb >= nsamp) break;
+                }
+            }
+        }
+#endif
         __syncthreads();
         // fold the circular orientation bins and convert; lane holds dst[lane], dst[lane+64]
         float dv[2];
@@ -1668,11 +1847,24 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
             const int ci = cell / DW, cj = cell - ci * DW;
             const int base = ((ci + 1) * (DW + 2) + (cj + 1)) * DBS;
             uint32_t v = 0;
+#if VO_DESC_PAIR
+            const int cbase = ((ci + 1) * (DW + 2) + (cj + 1)) * DN;
+#pragma unroll
+            for (int cp = 0; cp < DCOPIES; ++cp) {
+                v += hfx[2 * (cp * DCS2 + cbase + ob)];                              // low word: bin ob
+                v += hfx[2 * (cp * DCS2 + cbase + ((ob + DN - 1) & (DN - 1))) + 1];  // high word of ob-1
+            }
+            (void)base;
+#else
 #pragma unroll
             for (int cp = 0; cp < DCOPIES; ++cp) {
                 v += hfx[cp * DCS + base + ob];
                 if (ob == 0) v += hfx[cp * DCS + base + DN];
             }
+#endif
+#if VO_DESC_DIAG_NOATOMIC
+            v += diag & 1u;
+#endif
             dv[h] = vo_desc_fx_to_float(v);
         }
         float s = dv[0] * dv[0] + dv[1] * dv[1];
@@ -1975,7 +2167,7 @@ void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const v
     VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, b.n_cand, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
                        n_img, p.upsample);
     // 4 histogram copies: 2 -> +4 %, 8 -> +33 % k_desc time (MI355X)
-    VO_LAUNCH_NAMED("k_desc", (k_desc<4>), dim3(kFeatureGrid), dim3(64), 0, s, d_py, A, b.kpi, b.n_kp, b.desc,
+    VO_LAUNCH_NAMED("k_desc", (k_desc<VO_DESC_COPIES>), dim3(kFeatureGrid), dim3(64), 0, s, d_py, A, b.kpi, b.n_kp, b.desc,
                     b.meta, b.kp_cap, n_img);
 }
 

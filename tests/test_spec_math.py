@@ -15,6 +15,11 @@ def test_expf_accuracy(oracle):
     assert oracle.spec_eval("expf", np.array([-100.0]))[0] == 0.0
 
 
+def test_expf_nonpos_equals_expf_exhaustively(oracle):
+    # the HIP window weights (k_orient, k_desc) use the ldexp form on [-87, 0]
+    assert oracle.spec_check_expf_nonpos() == 0
+
+
 def test_atan2_deg_accuracy(oracle):
     rng = np.random.default_rng(0)
     y = rng.uniform(-300, 300, 20000)
