@@ -1357,6 +1357,10 @@ __global__ __launch_bounds__(64) void k_orient(const Pyramid* __restrict__ py, c
         __syncthreads();
         const int side = 2 * radius + 1, nsamp = side * side;
         const float inv_side = 1.0f / (float)side;          // (s + 0.5) * inv_side is exact enough to floor (s < 2^22)
+        // gradient loads through a buffer resource based at gim - P - 1: one 32-bit lane offset
+        // (the window row as a 24-bit multiply of the clamped row step), row y as one 12-B load
+        const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)(gim - P - 1), 0, 0x7FFFFFF0, 0x00020000);
+        const int c_off = r * P + c;                      // wave-uniform
         constexpr int U = 4;
         for (int s0 = lane; s0 < nsamp; s0 += 64 * U) {
             float gx[U], gy[U];
@@ -1365,29 +1369,33 @@ __global__ __launch_bounds__(64) void k_orient(const Pyramid* __restrict__ py, c
 #pragma unroll
             for (int q = 0; q < U; ++q) {                 // indices, bounds, gradient loads
                 const int s = s0 + 64 * q;
-                const int iq = (int)(((float)s + 0.5f) * inv_side);
-                const int i = iq - radius, j = s - iq * side - radius;
+                const float sf = (float)s, iqf = truncf((sf + 0.5f) * inv_side);
+                const int i = (int)iqf - radius, j = (int)(sf - iqf * (float)side) - radius;   // exact: < 2^24
                 const int y = r + i, x = c + j;
                 ii[q] = i; jj[q] = j;
-                okk[q] = s < nsamp && y > 0 && y < rows - 1 && x > 0 && x < cols - 1;
-                // every lane loads (clamped to the interior, weight masked below): no branches,
-                // 32-bit offsets from the wave-uniform plane base
-                const int yc = min(max(y, 1), rows - 2), xc = min(max(x, 1), cols - 2);
-                const uint32_t o = (uint32_t)(yc * P + xc);
-                gx[q] = gim[o + 1] - gim[o - 1];
-                gy[q] = gim[o - P] - gim[o + P];
+                okk[q] = (s < nsamp) & (y > 0) & (y < rows - 1) & (x > 0) & (x < cols - 1);
+                // every lane loads (clamped to the interior, weight masked below): no branches
+                const int ic = min(max(i, 1 - r), rows - 2 - r), jc = min(max(j, 1 - c), cols - 2 - c);
+                const int vo = 4 * (c_off + __mul24(ic, P) + jc);
+                typedef int i3_t __attribute__((ext_vector_type(3)));
+                const i3_t h = __builtin_amdgcn_raw_buffer_load_b96(grs, vo, 4 * P, 0);
+                gx[q] = __int_as_float(h.z) - __int_as_float(h.x);
+                gy[q] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 0, 0)) -
+                        __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 8 * P, 0));
             }
 #pragma unroll
             for (int q = 0; q < U; ++q) {
                 const float dx = gx[q], dy = gy[q];
-                float w = vo_expf_nonpos((float)(ii[q] * ii[q] + jj[q] * jj[q]) * expf_scale);   // arg in [-21, 0]
+                const float fi = (float)ii[q], fj = (float)jj[q];            // i^2 + j^2 exact in float
+                float w = vo_expf_nonpos((fi * fi + fj * fj) * expf_scale);   // arg in [-21, 0]
                 float mag = vo_grad_mag(dx, dy);
                 float ori = vo_atan2_deg(dy, dx);
-                int bin = vo_round((float)VO_SIFT_ORI_BINS / 360.0f * ori);
+                int bin = vo_round((float)VO_SIFT_ORI_BINS / 360.0f * ori);   // ori in [0, 360): bin in [0, 36]
                 if (bin >= VO_SIFT_ORI_BINS) bin -= VO_SIFT_ORI_BINS;
-                if (bin < 0) bin += VO_SIFT_ORI_BINS;
                 const uint32_t qv = vo_desc_fx_quant((w * mag) * VO_DESC_FX_SCALE);
-                hp[bin * 64 + lane] += okk[q] ? qv : 0u;          // private column, bank = lane; masked samples add 0
+                // private column, bank = lane; masked samples add 0; a returnless LDS add, so the
+                // update does not wait for the column's old value
+                atomicAdd(&hp[bin * 64 + lane], okk[q] ? qv : 0u);
             }
         }
         __syncthreads();
