@@ -590,6 +590,13 @@ static SetRef set_ref(vo_ctx* c, int set)
 // features of part k overlap the scale space of part k+1 (and of the next call, which uses
 // the other set).  Inputs are ordered after earlier work on `stream`; the set's previous
 // contents are released by its ev_done.  With `join`, `stream` waits for the result.
+// Where the extremum test of octaves 1.. runs: 1 (default) on the feature stream after the
+// scale space, 0 at the scale space's tail.  With the faster k_desc / k_orient of round 3 the
+// scale-space stream became the critical path again, and moving that 0.4 ms of test off it
+// gave 7.51-7.55 vs 7.66-7.77 ms per 64-frame step (A/B on one box).
+#ifndef VO_EXT_SPLIT
+#define VO_EXT_SPLIT 1
+#endif
 static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uint8_t* d_r, int B, bool join,
                                bool fork = true)
 {
@@ -603,14 +610,14 @@ static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uin
     }
     HIPC(c, hipStreamWaitEvent(sp, c->ev_done[set], 0));      // set free (its previous features done)
     // scale space on sp; octave 0's extremum test on st as soon as octave 0 is built (beside the
-    // scale space of octaves 1..), the other octaves' at the scale space's tail -- the split
-    // that balances the two streams
+    // scale space of octaves 1..), the other octaves' on st after the scale space (VO_EXT_SPLIT)
+    // -- the split that balances the two streams
     for (int p = 0; p < parts; ++p) {
         const int f0 = B * p / parts, nf = B * (p + 1) / parts - f0;
         ImageSrc src{d_l + f0 * fs, d_r + f0 * fs, fs, c->cols, 0};
         SiftBuffers v = sift_view(*S.sb, c->py, 2 * f0, 2 * nf);
         sift_enqueue_pyramid(c->py, v, src, 2 * nf, c->sp, sp, c->d_py, c->ev_o0[p]);
-        sift_enqueue_pyramid_tail(c->py, v, 2 * nf, c->sp, sp, c->d_py, 1);
+        sift_enqueue_pyramid_tail(c->py, v, 2 * nf, c->sp, sp, c->d_py, VO_EXT_SPLIT ? c->py.n_oct : 1);
         HIPC(c, hipEventRecord(c->ev_join[p], sp));
     }
     for (int p = 0; p < parts; ++p) {
@@ -621,6 +628,7 @@ static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uin
         HIPC(c, hipStreamWaitEvent(st, c->prof.on && join ? c->ev_join[p] : c->ev_o0[p], 0));
         sift_enqueue_extrema(c->py, v, 2 * nf, c->sp, st, c->d_py, 0, 1);
         HIPC(c, hipStreamWaitEvent(st, c->ev_join[p], 0));
+        if (VO_EXT_SPLIT) sift_enqueue_extrema(c->py, v, 2 * nf, c->sp, st, c->d_py, 1, c->py.n_oct);
         sift_enqueue_features(c->py, v, 2 * nf, c->sp, st, c->d_py);
         match_launch(match_view(*S.mb, f0), S.jobs + f0, nf, c->mp, st);
     }
