@@ -48,6 +48,7 @@ void build_pyramid_geometry(Pyramid& py, int rows, int cols, int n_img, const vo
         OctGeom& g = py.oct[o];
         if (o) { R /= 2; C /= 2; }
         g.rows = R; g.cols = C;
+        g.dmax = (int)sqrt((double)C * C + (double)R * R);
         g.pitch = (C + 255) / 256 * 256;    // whole 256-column blur strips: masked-off lanes store into padding
         g.plane = (size_t)g.rows * g.pitch;
         for (int i = 0; i < L + 3; ++i) { g.g_off[i] = off; off += g.plane; }
@@ -1540,6 +1541,9 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
 #ifndef VO_DESC_U
 #define VO_DESC_U 2               // blocks of 64 samples per batch (VO_DESC_LOOP 1)
 #endif
+#ifndef VO_DESC_MARGIN
+#define VO_DESC_MARGIN 0          // extra columns around the descriptor rows' real-arithmetic bounds
+#endif
 #ifndef VO_DESC_ADDR
 #define VO_DESC_ADDR 1            // 1: buffer gradient loads from one 32-bit offset, 24-bit index multiplies
 #endif
@@ -1590,8 +1594,7 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
         const float exp_scale = -1.0f / ((float)(DW * DW) * 0.5f);
         const float hist_width = VO_SIFT_DESCR_SCL * q.scl;
         int radius = vo_round(hist_width * 1.4142135623730951f * (float)(DW + 1) * 0.5f);
-        const int rmax = (int)sqrt((double)cols * cols + (double)rows * rows);
-        if (radius > rmax) radius = rmax;
+        if (radius > g.dmax) radius = g.dmax;
         if (radius > VO_SIFT_DESCR_RMAX) radius = VO_SIFT_DESCR_RMAX;
         cos_t = cos_t / hist_width;
         sin_t = sin_t / hist_width;
@@ -1609,20 +1612,21 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
             if (r <= 0 || r >= rows - 1) { jlo = 1; jhi = 0; }
             else {
                 // |j*ct - i*st| < lim  and  |j*st + i*ct| < lim  (rbin = r_rot + 1.5 in (-1, DW)); lim is
-                // 1e-3 bin widths wider than the test below and the bounds get one column of margin,
-                // far above the float error of these products (< 1e-4 columns at r <= RMAX)
+                // 1e-3 bin widths wider than the test below, far above the float error of the test
+                // (~1e-6) and of these bounds (< 1e-4 columns at r <= RMAX), so [floor(a), ceil(b)]
+                // holds every accepted column (VO_DESC_MARGIN extra columns of margin)
                 const float fi = (float)i, lim = 0.5f * DW + 0.5f + 1e-3f, cap = (float)(radius + 2);
                 if (fabsf(cos_t) > 1e-9f) {
                     float a = (fi * sin_t - lim) * inv_ct, b = (fi * sin_t + lim) * inv_ct;
                     if (a > b) { const float t2 = a; a = b; b = t2; }
                     a = fminf(fmaxf(a, -cap), cap); b = fminf(fmaxf(b, -cap), cap);
-                    jlo = max(jlo, (int)floorf(a) - 1); jhi = min(jhi, (int)ceilf(b) + 1);
+                    jlo = max(jlo, (int)floorf(a) - VO_DESC_MARGIN); jhi = min(jhi, (int)ceilf(b) + VO_DESC_MARGIN);
                 } else if (fabsf(fi * sin_t) >= lim) { jlo = 1; jhi = 0; }
                 if (fabsf(sin_t) > 1e-9f) {
                     float a = (-fi * cos_t - lim) * inv_st, b = (-fi * cos_t + lim) * inv_st;
                     if (a > b) { const float t2 = a; a = b; b = t2; }
                     a = fminf(fmaxf(a, -cap), cap); b = fminf(fmaxf(b, -cap), cap);
-                    jlo = max(jlo, (int)floorf(a) - 1); jhi = min(jhi, (int)ceilf(b) + 1);
+                    jlo = max(jlo, (int)floorf(a) - VO_DESC_MARGIN); jhi = min(jhi, (int)ceilf(b) + VO_DESC_MARGIN);
                 } else if (fabsf(fi * cos_t) >= lim) { jlo = 1; jhi = 0; }
                 jlo = max(jlo, 1 - px); jhi = min(jhi, cols - 2 - px);
                 // trim the superset to the exact set: the float test below is monotone

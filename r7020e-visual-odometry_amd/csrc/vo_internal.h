@@ -55,7 +55,7 @@ extern Profiler* g_prof;
 // ---------------------------------------------------------------------------
 struct OctGeom {
     int rows, cols, pitch;
-    int pad;
+    int dmax;                           // descriptor window radius cap, (int)sqrt(cols^2 + rows^2)
     size_t plane;                       // rows * pitch (floats)
     size_t g_off[VO_SIFT_MAX_LAYERS];   // L+3 Gaussian levels
 };
