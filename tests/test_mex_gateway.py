@@ -60,6 +60,7 @@ def test_sift_hands_over_column_major_image(mex):
 
 
 def test_sift_new_size_replaces_context(mex):
+    mex.call("sift", np.zeros((20, 30), np.uint8))      # a context of another size exists first
     c0, d0 = mex.i("creates"), mex.i("destroys")
     mex.call("sift", np.zeros((24, 30), np.uint8))
     assert mex.i("creates") == c0 + 1 and mex.i("destroys") == d0 + 1
