@@ -1738,7 +1738,6 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
         // the gradient neighbours of a listed sample (every listed sample is interior): x+1, x-1 as
         // one 12-B load (through a 3-float type declared with the 4-B alignment the address has),
         // y-1, y+1
-        typedef float f3u_t __attribute__((ext_vector_type(3), aligned(4)));
 #if VO_DESC_ADDR
         // buffer loads with one 32-bit lane offset: the resource starts at the sample's row y-1
         // column x-1 for offset 0 (gim - P - 1), so row y-1 is +4 B, row y (x-1..x+1) +4P B and
@@ -1759,6 +1758,7 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
             g4[2] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 0, 0));
             g4[3] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 8 * P, 0));
 #else
+            typedef float f3u_t __attribute__((ext_vector_type(3), aligned(4)));
             const float* gp = gim + (uint32_t)((pyy + i) * P + px + j);   // 32-bit offset from the uniform base
             const f3u_t h = *reinterpret_cast<const f3u_t*>(gp - 1);
             g4[0] = h.z; g4[1] = h.x;
@@ -1969,7 +1969,10 @@ static bool launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
 #ifndef VO_BLUR_MAX_TH
 #define VO_BLUR_MAX_TH 128
 #endif
-        constexpr int kMaxTH = VO_BLUR_MAX_TH, kWaveTarget = 2048, kCpl2MaxC = VO_CPL2_MAXC;
+#ifndef VO_BLUR_WAVES
+#define VO_BLUR_WAVES 2048
+#endif
+        constexpr int kMaxTH = VO_BLUR_MAX_TH, kWaveTarget = VO_BLUR_WAVES, kCpl2MaxC = VO_CPL2_MAXC;
         const bool base = name[7] == 'b';
         const int cpl = (!base && C <= kCpl2MaxC) ? 2 : 4;
         const int n_strips = (C + 64 * cpl - 1) / (64 * cpl);
