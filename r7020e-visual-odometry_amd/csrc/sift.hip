@@ -927,6 +927,11 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
     for (int lv = 0; lv < NG; ++lv) goff[lv] = g.g_off[lv];
     const int wr = py->wrow[o];
     unsigned long long* mrow = mask + (size_t)img * py->n_words;
+#if VO_EXT_BSTORE
+    // mask words by buffer stores issued by every lane every row: lanes other than 0/1 (and rows
+    // past the band) get an out-of-range offset and the hardware drops them -- no store branch
+    const __amdgpu_buffer_rsrc_t rs_m = __builtin_amdgcn_make_buffer_rsrc(mrow, 0, py->n_words * 8, 0x00020000);
+#endif
     int wb[L];                                       // mask word base per layer, hoisted: the mask
 #pragma unroll                                       // stores could alias *py for the compiler
     for (int l = 0; l < L; ++l) wb[l] = py->wbase[o * L + l];
@@ -998,8 +1003,14 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
                 }
                 const uint64_t w0 = __ballot(e[0] & in0), w1 = __ballot(e[1] & in1);
                 const int k = 2 * strip + lane;               // wr is even: both words exist
+#if VO_EXT_BSTORE
+                const uint32_t mo = (lane < 2 && t - 2 < nrow) ? (uint32_t)(wb[layer - 1] + (r - VO_SIFT_BORDER) * wr + k) * 8u
+                                                               : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(vo_i2, (uint64_t)(lane ? w1 : w0)), rs_m, mo, 0, 0);
+#else
                 if (lane < 2 && t - 2 < nrow)
                     mrow[wb[layer - 1] + (size_t)(r - VO_SIFT_BORDER) * wr + k] = lane ? w1 : w0;
+#endif
             }
         }
     };

@@ -83,6 +83,9 @@ struct Pyramid {
 #ifndef VO_EXT_BAND
 #define VO_EXT_BAND 30            // interior rows per extremum-test wave (a multiple of 3)
 #endif
+#ifndef VO_EXT_BSTORE
+#define VO_EXT_BSTORE 1           // extremum test: mask words by unconditional buffer stores (0: branchy stores)
+#endif
 #define VO_SEG_WORDS 1024
 
 // Packed candidate: c | r << 12 | layer << 24 | o << 27  (c, r < 4096)
