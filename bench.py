@@ -50,7 +50,8 @@ TRAFFIC_FILE = max(ROOT.glob("profiles/r*_pmc_traffic.json"), default=ROOT / "pr
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=20, help="timed steps per run (64 frames each: 1280 frames per run)")
+    ap.add_argument("--runs", type=int, default=5, help="timed runs of --steps steps; value = the median run (SURVEY §8d)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64, help="stereo frames per step")
     ap.add_argument("--cpu-frames", type=int, default=32, help="frames in the CPU-oracle baseline sample")
@@ -217,9 +218,23 @@ def main():
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": world}))
         return
+    # VO_BENCH_FORCE_DIST=1: take the process-group branch (RCCL with the default backend) even
+    # at one rank -- the only way this pool can run the collectives on hardware before an
+    # 8-GPU node is available (env rendezvous on 127.0.0.1 when no launcher set it)
+    force_dist = os.environ.get("VO_BENCH_FORCE_DIST") == "1"
+    if force_dist and world == 1:
+        import socket
+        if "MASTER_PORT" not in os.environ:
+            s_ = socket.socket()
+            s_.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(s_.getsockname()[1])
+            s_.close()
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if world > 1 or force_dist:
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -257,17 +272,47 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ctx.sift_match_batch_dev(d_l.data_ptr(), d_r.data_ptr(), B, stats=False)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    barrier()
-    elapsed = max_over_ranks(elapsed)
+    # --runs timed runs of exactly --steps steps each, every run bracketed by a barrier +
+    # synchronize and reduced max-over-ranks; value = the median run (median of 5)
+    run_s = []
+    for _ in range(max(1, args.runs)):
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            ctx.sift_match_batch_dev(d_l.data_ptr(), d_r.data_ptr(), B, stats=False)
+        torch.cuda.synchronize()
+        el_ = time.perf_counter() - t0
+        barrier()
+        run_s.append(max_over_ranks(el_))
+    elapsed = sorted(run_s)[len(run_s) // 2]
     frames = B * args.steps * world
     fps = frames / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+    timed_runs = {"n": len(run_s), "steps_per_run": args.steps, "frames_per_run": frames,
+                  "ms_per_step": [round(x / args.steps * 1e3, 4) for x in run_s],
+                  "value_median": fps, "value_min": frames / max(run_s), "value_max": frames / min(run_s)}
+
+    # H2D of one batch of u8 pairs (pinned host -> HBM), reported beside `value` (which starts
+    # from resident inputs): the PCIe-inclusive rate if the frames came from the host each step
+    hl = torch.from_numpy(L).pin_memory()
+    hr = torch.from_numpy(R).pin_memory()
+    h2d_ms = []
+    for _ in range(6):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        d_l.copy_(hl, non_blocking=True)
+        d_r.copy_(hr, non_blocking=True)
+        e1.record()
+        e1.synchronize()
+        h2d_ms.append(e0.elapsed_time(e1))
+    h2d = sorted(h2d_ms[1:])[len(h2d_ms[1:]) // 2]
+    h2d_bytes = 2 * B * ROWS * COLS
+    del hl, hr
+    h2d_line = {"bytes_per_step": h2d_bytes, "ms_per_step": h2d, "gb_s": h2d_bytes / (h2d * 1e-3) / 1e9,
+                "frames_per_s_serial": B / ((ms_per_step + h2d) * 1e-3),
+                "frames_per_s_overlapped": B / (max(ms_per_step, h2d) * 1e-3),
+                "note": "pinned host -> HBM copy of the step's 2x64 u8 images (torch, one stream), median of 5; "
+                        "serial = copy then compute, overlapped = copy of step N+1 beside compute of step N"}
 
     # ---- per-kernel HIP-event durations on libvo's streams (separate passes) ----
     # in situ: calls issued back to back exactly like the timed loop (the scale space of
@@ -400,12 +445,14 @@ def main():
         line = {
             "metric": "stereo frames/sec @1242x375 (SIFT detect+describe x2 + stereo matchFeatures)",
             "value": fps, "unit": "stereo frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "ms_per_step": ms_per_step, "timed_runs": timed_runs, "h2d": h2d_line,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32 (i8 MFMA for exact descriptor dot products)", "data": "synthetic",
             "config": {"workload": "BASELINE configs[1]: SIFT detect+describe + BF match on 1242x375 synthetic stereo, "
                                    "~2k keypoints/image", "frames_per_step_per_gpu": B, "rows": ROWS, "cols": COLS,
                        "mean_keypoints_per_image": float(kp), "mean_stereo_matches": float(st),
-                       "parallelism": f"frames sharded over {world} GPU(s)"},
+                       "parallelism": f"frames sharded over {world} GPU(s)",
+                       "process_group": dist.get_backend() if dist is not None else None},
             "roofline": roof,
             "cpu_baseline": cpu,
             "full_path": full,

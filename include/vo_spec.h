@@ -96,12 +96,48 @@ VO_HD float vo_expf_nonpos(float x)
 }
 
 /* ------------------------------------------------------------------------ */
+/* Reciprocal of d in [2^-100, 2^100] by an integer seed and three Newton    */
+/* steps r <- r + r (1 - d r), each two fmaf: basic ops only, so GPU == CPU  */
+/* bit for bit.  The seed 0x7EF311C3 - bits(d) is within 12.5 % of 1/d; the  */
+/* steps square the relative error (1.6e-2, 2.4e-4, 6e-8), so the result is  */
+/* within ~2 ulp of 1/d (pinned against 1/d in tests/test_spec_math.py).     */
+/* On gfx950 it is 7 full-rate VALU ops against the IEEE division's 11, one  */
+/* of them the quarter-rate v_rcp_f32.                       */
+/* ------------------------------------------------------------------------ */
+VO_HD float vo_rcp_nr(float d)
+{
+    float r = vo_u32_as_f32(0x7EF311C3u - vo_f32_as_u32(d));
+    float e = fmaf(-d, r, 1.0f);
+    r = fmaf(r, e, r);
+    e = fmaf(-d, r, 1.0f);
+    r = fmaf(r, e, r);
+    e = fmaf(-d, r, 1.0f);
+    return fmaf(r, e, r);
+}
+
+/* ------------------------------------------------------------------------ */
+/* SIFT window weights, separable.  OpenCV weighs an orientation sample by   */
+/* exp((i^2 + j^2) s) and a descriptor sample by exp((c_rot^2 + r_rot^2) s)  */
+/* with c_rot^2 + r_rot^2 = (i^2 + j^2) / hist_width^2 (a rotation).  The    */
+/* spec takes the product of the two one-dimensional factors,                */
+/*   w(i, j) = vo_sift_wt(s, |i|) * vo_sift_wt(s, |j|),                      */
+/* equal in exact arithmetic and within float rounding of OpenCV's value,    */
+/* so the kernels read both factors from a per-keypoint table of radius + 1  */
+/* entries instead of evaluating an exp per sample.  k^2 s must lie in       */
+/* [-87, 0] (vo_expf_nonpos): at most ~5 for the orientation window, ~1.6    */
+/* for the descriptor's rotated square.                                      */
+/* ------------------------------------------------------------------------ */
+VO_HD float vo_sift_wt(float s, int k) { return vo_expf_nonpos((float)(k * k) * s); }
+
+/* ------------------------------------------------------------------------ */
 /* atan2 in DEGREES, result in [0, 360).  (OpenCV fastAtan2 convention:      */
 /* angle of the vector (x, y), counter-clockwise from +x.)  Accurate to      */
-/* ~1e-5 deg; only basic ops.  Written select-only with ONE division so the  */
-/* SIMT form has no divergent branches: with lo = min(|x|,|y|), hi = max,    */
+/* ~1e-5 deg; only basic ops.  Written select-only with ONE reciprocal so    */
+/* the SIMT form has no divergent branches: with lo = min(|x|,|y|), hi = max,*/
 /*   t = lo/hi            if lo <= tan(pi/8)*hi  (tested as a float product) */
-/*   t = (lo-hi)/(lo+hi)  otherwise, and atan(lo/hi) = pi/4 + atan(t).       */
+/*   t = (lo-hi)/(lo+hi)  otherwise, and atan(lo/hi) = pi/4 + atan(t),       */
+/* the quotient formed as num * vo_rcp_nr(den) (den clamped to >= 1e-30:    */
+/* |num| <= den, so |t| <= 1 everywhere and t = 0 at the origin).            */
 /* ------------------------------------------------------------------------ */
 VO_HD float vo_atan2_deg(float y, float x)
 {
@@ -111,7 +147,7 @@ VO_HD float vo_atan2_deg(float y, float x)
     const int red = lo > 0.41421356f * hi;
     const float num = red ? lo - hi : lo;
     const float den = red ? lo + hi : hi;
-    const float t = num / (den > 0.0f ? den : 1.0f);      /* origin: num = 0 -> t = 0 */
+    const float t = num * vo_rcp_nr(den > 1e-30f ? den : 1e-30f);
     const float t2 = t * t;
     /* odd Taylor series to t^15, |t| <= tan(pi/8) -> truncation < 2e-8 */
     float p = -1.0f / 15.0f;
@@ -292,7 +328,7 @@ VO_HD float vo_hist_fx_to_float(uint64_t s) { return (float)s * (1.0f / VO_DESC_
 #define VO_SIFT_DESCR_SCL 3.0f
 #define VO_SIFT_DESCR_MAG_THR 0.2f
 #define VO_SIFT_DESCR_INT_FCTR 512.0f
-#define VO_SIFT_DESCR_RMAX 128     /* descriptor window radius cap (38 at the defaults) */
+#define VO_SIFT_DESCR_RMAX 127     /* descriptor window radius cap (38 at the defaults); (2 RMAX + 1)^2 < 2^16 */
 #define VO_SIFT_MAX_PEAKS 18      /* strict local maxima in a 36-bin circle */
 #define VO_FLT_EPSILON 1.19209290e-07f
 

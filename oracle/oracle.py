@@ -296,7 +296,7 @@ def sift_match_pair(left, right, sp=None, mp=None):
     return S, nl.value, nr.value
 
 
-SPEC_FN = {"expf": 0, "atan2_deg": 1, "sin_deg": 2, "cos_deg": 3, "exp_d": 4, "log_d": 5}
+SPEC_FN = {"expf": 0, "atan2_deg": 1, "sin_deg": 2, "cos_deg": 3, "exp_d": 4, "log_d": 5, "rcp_nr": 6, "sift_wt": 7}
 
 
 def spec_check_expf_nonpos() -> int:
@@ -307,7 +307,7 @@ def spec_check_expf_nonpos() -> int:
 def spec_eval(fn: str, x) -> np.ndarray:
     """Evaluate a vo_spec.h primitive (float ones are computed in float)."""
     x = np.ascontiguousarray(x, np.float64).reshape(-1)
-    n = x.shape[0] // 2 if fn == "atan2_deg" else x.shape[0]   # atan2 takes (y, x) pairs
+    n = x.shape[0] // 2 if fn in ("atan2_deg", "sift_wt") else x.shape[0]   # atan2: (y, x) pairs; sift_wt: (s, k)
     out = np.zeros(n)
     lib().oracle_spec_eval(SPEC_FN[fn], _p(x, C.c_double), _p(out, C.c_double), n)
     return out

@@ -293,6 +293,9 @@ static int orientations(const float* img, int rows, int cols, int r, int c, floa
 #else
     uint64_t hfx[VO_SIFT_ORI_BINS];
     memset(hfx, 0, sizeof(hfx));
+    /* separable window weight (vo_spec.h vo_sift_wt): w(i, j) = wt[|i|] * wt[|j|] */
+    float* wt = (float*)malloc(sizeof(float) * (size_t)(radius + 1));
+    for (int k = 0; k <= radius; ++k) wt[k] = vo_sift_wt(expf_scale, k);
 #endif
     for (int i = -radius; i <= radius; ++i) {
         int y = r + i;
@@ -302,7 +305,11 @@ static int orientations(const float* img, int rows, int cols, int r, int c, floa
             if (x <= 0 || x >= cols - 1) continue;
             float dx = AT(img, cols, y, x + 1) - AT(img, cols, y, x - 1);
             float dy = AT(img, cols, y - 1, x) - AT(img, cols, y + 1, x);
+#ifdef VO_CV_LITERAL
             float w = SIFT_EXPF((float)(i * i + j * j) * expf_scale);
+#else
+            float w = wt[i < 0 ? -i : i] * wt[j < 0 ? -j : j];
+#endif
             float mag = sqrtf(dx * dx + dy * dy);
             float ori = SIFT_ATAN2(dy, dx);
             int bin = vo_round((float)n / 360.0f * ori);
@@ -319,6 +326,7 @@ static int orientations(const float* img, int rows, int cols, int r, int c, floa
 #ifdef VO_CV_LITERAL
     for (int k = 0; k < n; ++k) t[k] = hfl[k];
 #else
+    free(wt);
     for (int k = 0; k < n; ++k) t[k] = vo_hist_fx_to_float(hfx[k]);
 #endif
     float maxval = 0.0f;
@@ -373,6 +381,13 @@ static void descriptor(const float* img, int rows, int cols, float xo, float yo,
 #endif
     cos_t = cos_t / hist_width;
     sin_t = sin_t / hist_width;
+#ifndef VO_CV_LITERAL
+    /* separable window weight (vo_spec.h vo_sift_wt): exp((c_rot^2 + r_rot^2) exp_scale) =
+     * exp(i^2 s) exp(j^2 s), s = exp_scale / hist_width^2 -- w(i, j) = wt[|i|] * wt[|j|] */
+    const float wsc = exp_scale / (hist_width * hist_width);
+    float wt[VO_SIFT_DESCR_RMAX + 1];
+    for (int k = 0; k <= radius; ++k) wt[k] = vo_sift_wt(wsc, k);
+#endif
     hist_t hfx[(VO_SIFT_DESCR_W + 2) * (VO_SIFT_DESCR_W + 2) * (VO_SIFT_DESCR_BINS + 2)];
     memset(hfx, 0, sizeof(hfx));
     for (int i = -radius; i <= radius; ++i) {
@@ -386,7 +401,11 @@ static void descriptor(const float* img, int rows, int cols, float xo, float yo,
                   r > 0 && r < rows - 1 && c > 0 && c < cols - 1)) continue;
             float dx = AT(img, cols, r, c + 1) - AT(img, cols, r, c - 1);
             float dy = AT(img, cols, r - 1, c) - AT(img, cols, r + 1, c);
+#ifdef VO_CV_LITERAL
             float w = SIFT_EXPF((c_rot * c_rot + r_rot * r_rot) * exp_scale);
+#else
+            float w = wt[i < 0 ? -i : i] * wt[j < 0 ? -j : j];
+#endif
             float ang = SIFT_ATAN2(dy, dx);
 #ifdef VO_CV_LITERAL
             float mag = sqrtf(dx * dx + dy * dy) * w;

@@ -5,7 +5,8 @@
 #include <stdint.h>
 #include "vo_spec.h"
 
-/* fn: 0 expf, 1 atan2_deg(y=in[2i], x=in[2i+1]), 2 sin_deg, 3 cos_deg, 4 exp_d, 5 log_d */
+/* fn: 0 expf, 1 atan2_deg(y=in[2i], x=in[2i+1]), 2 sin_deg, 3 cos_deg, 4 exp_d, 5 log_d,
+ *     6 rcp_nr, 7 sift_wt(s=in[2i], k=in[2i+1]) */
 void oracle_spec_eval(int fn, const double* in, double* out, int n)
 {
     for (int i = 0; i < n; ++i) {
@@ -16,6 +17,8 @@ void oracle_spec_eval(int fn, const double* in, double* out, int n)
         case 3: { float s, c; vo_sincos_deg((float)in[i], &s, &c); out[i] = c; break; }
         case 4: out[i] = vo_exp_d(in[i]); break;
         case 5: out[i] = vo_log_d(in[i]); break;
+        case 6: out[i] = vo_rcp_nr((float)in[i]); break;
+        case 7: out[i] = vo_sift_wt((float)in[2 * i], (int)in[2 * i + 1]); break;
         default: out[i] = 0; break;
         }
     }

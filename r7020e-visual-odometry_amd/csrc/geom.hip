@@ -5,12 +5,14 @@
 //       next step's lists, so no descriptor is ever copied.
 //   triangulate (VO.m:113-116)            k_gather_tri: one lane per tracked
 //       point, linear DLT + one-sided Jacobi SVD in f64 (oracle dlt_point).
-//   estworldpose (VO.m:123-127)           k_msac_hyp: one lane per hypothesis
-//       slot (Philox sample, Grunert P3P, 4th-point disambiguation);
-//       k_msac_score: one wave per hypothesis (lane-strided partial MSAC sums +
-//       fixed shuffle tree); k_msac_select: the sequential adaptive-termination
-//       loop replayed on the precomputed slots (one lane per frame);
-//       k_msac_final: inlier mask + camera pose.
+//   estworldpose (VO.m:123-127)           k_msac: one block per frame walks the
+//       hypothesis slots in chunks of 64 -- a lane per slot (Philox sample,
+//       Grunert P3P, 4th-point disambiguation), a wave per slot score
+//       (lane-strided partial MSAC sums + fixed shuffle tree), then the
+//       sequential adaptive-termination replay of the chunk -- until the replay
+//       stops; msac_final: inlier mask + camera pose.  (The eager kernels
+//       k_msac_hyp / k_msac_score / k_msac_select score every slot first; they
+//       are compiled only into the test build libvo_exp.so, VO_EXPERIMENTAL.)
 //   landmarks (VO.m:145-160, CreateLandmarksFromFeatures.m)  k_lm_filter
 //       (any-x-or-y equality test, quirk Q3) + block compaction, k_lm_tri (odd
 //       rows, z gates).  The world transform needs the chained pose and runs
@@ -493,6 +495,7 @@ __device__ void msac_hyp_slot(const MsacArgs& a, int f, int s, int n)
     h->valid = 1;
 }
 
+#if VO_EXPERIMENTAL   // eager MSAC: test build only (libvo_exp.so), the cross-check of k_msac
 // one lane per (frame, slot).  grid (ceil(n_hyp/64), B)  (eager form: every slot)
 __global__ __launch_bounds__(64) void k_msac_hyp(MsacArgs a)
 {
@@ -501,6 +504,7 @@ __global__ __launch_bounds__(64) void k_msac_hyp(MsacArgs a)
     if (s >= a.n_hyp) return;
     msac_hyp_slot(a, f, s, msac_n(a, f));
 }
+#endif  // VO_EXPERIMENTAL
 
 // MSAC score of one valid slot by one wave: 64 lane-strided partials + the fixed shuffle tree
 __device__ __forceinline__ void msac_score_slot(const MsacArgs& a, int f, int s, int n, int lane)
@@ -526,6 +530,7 @@ __device__ __forceinline__ void msac_score_slot(const MsacArgs& a, int f, int s,
     if (lane == 0) { h->score = part; h->n_in = cnt; }
 }
 
+#if VO_EXPERIMENTAL   // eager MSAC: test build only (libvo_exp.so), the cross-check of k_msac
 // one wave per (frame, slot): MSAC score = 64 lane-strided partials + tree
 __global__ __launch_bounds__(256) void k_msac_score(MsacArgs a, int B)
 {
@@ -537,6 +542,7 @@ __global__ __launch_bounds__(256) void k_msac_score(MsacArgs a, int B)
         msac_score_slot(a, f, s, msac_n(a, f), lane);
     }
 }
+#endif  // VO_EXPERIMENTAL
 
 __device__ int msac_trials_needed_dev(int n_in, int n, double conf)
 {
@@ -554,6 +560,7 @@ __device__ int msac_trials_needed_dev(int n_in, int n, double conf)
 
 __device__ void msac_final(const MsacArgs& a, int f, int n, int best, int status, int lane);
 
+#if VO_EXPERIMENTAL   // eager MSAC: test build only (libvo_exp.so), the cross-check of k_msac
 // sequential MSAC replay (adaptive trial count) + final inliers/pose.  block 64 per frame
 __global__ __launch_bounds__(64) void k_msac_select(MsacArgs a)
 {
@@ -589,6 +596,7 @@ __global__ __launch_bounds__(64) void k_msac_select(MsacArgs a)
     __syncthreads();
     msac_final(a, f, n, s_best, s_status, lane);
 }
+#endif  // VO_EXPERIMENTAL
 
 // inlier mask + camera pose of the chosen slot (one wave)
 __device__ void msac_final(const MsacArgs& a, int f, int n, int best, int status, int lane)
@@ -849,18 +857,19 @@ static MsacArgs msac_args(GeomBuffers& g, const double* img, const double* world
 
 static void msac_enqueue(const MsacArgs& a, int B, hipStream_t s)
 {
-    // VO_MSAC_EAGER=1: the eager form (every slot generated and scored, then the replay) --
-    // kept as the cross-check of the lazy kernel (tests/test_gpu_geom.py)
-    const char* e = getenv("VO_MSAC_EAGER");
-    if (!(e && e[0] == '1')) {
-        VO_LAUNCH(k_msac, dim3(B), dim3(VO_MSAC_T), 0, s, a);
+#if VO_EXPERIMENTAL
+    // test build: the eager form (every slot generated and scored, then the replay) when
+    // vo_exp_set selects it -- the cross-check of the lazy kernel (tests/test_gpu_geometry.py)
+    if (g_exp_msac_eager) {
+        VO_LAUNCH(k_msac_hyp, dim3((a.n_hyp + 63) / 64, B), dim3(64), 0, s, a);
+        int blocks = (B * a.n_hyp + 3) / 4;
+        if (blocks > 4096) blocks = 4096;
+        VO_LAUNCH(k_msac_score, dim3(blocks), dim3(256), 0, s, a, B);
+        VO_LAUNCH(k_msac_select, dim3(B), dim3(64), 0, s, a);
         return;
     }
-    VO_LAUNCH(k_msac_hyp, dim3((a.n_hyp + 63) / 64, B), dim3(64), 0, s, a);
-    int blocks = (B * a.n_hyp + 3) / 4;
-    if (blocks > 4096) blocks = 4096;
-    VO_LAUNCH(k_msac_score, dim3(blocks), dim3(256), 0, s, a, B);
-    VO_LAUNCH(k_msac_select, dim3(B), dim3(64), 0, s, a);
+#endif
+    VO_LAUNCH(k_msac, dim3(B), dim3(VO_MSAC_T), 0, s, a);
 }
 
 void track_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_track_jobs, const StepArgs& a,

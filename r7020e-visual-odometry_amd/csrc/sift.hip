@@ -421,9 +421,20 @@ __device__ __forceinline__ void vo_dpp_window(const vec_t& vm, float* w)
 }
 
 
-// u8 source of the octave-0 base level (TAG & 4): the x2 upsample is formed
-// while staging each input row, from raw source words prefetched like floats.
+// u8 source of the octave-0 base level (TAG & 4): the x2 upsample is formed per input row from
+// source bytes the wave staged in LDS when it started (every source row its band reads, the
+// strip's byte columns).  The row loop then issues no vector-memory load at all: on gfx9 stores
+// and loads share one in-order vmcnt, so a row prefetched from HBM P steps ahead also waited for
+// the P steps of 16-B stores issued before it -- the base kernel's stream of 1 GB of stores was
+// paced by its tiny u8 loads.  With the loads gone the loop never waits on vmcnt.
 struct U8Src { const uint8_t* p; int ld, rows, cols; };
+constexpr int kBaseMaxTH = 128;                               // band height bound of the staged form
+// staged row length in dwords: the upsampled span of a wave (64 CPL columns + 2 RH halo) needs
+// (64 CPL + 2 RH) / 2 + 3 source bytes; + 3 for the row's misalignment, + 4 for the word pair
+__host__ __device__ constexpr int bs_u8_dw(int r, int cpl) { return ((64 * cpl + 2 * bs_rh(r, cpl)) / 2 + 3 + 3 + 4 + 3) / 4; }
+// staged rows: a band reads F + TH upsampled rows (F = 2r + E, E < P), i.e. at most half as many
+// source rows + 3 (the neighbour row of each end, rounding)
+__host__ __device__ constexpr int bs_u8_rows(int r) { return (2 * r + BS_P + kBaseMaxTH) / 2 + 4; }
 
 __device__ __forceinline__ vo_f4 up4_from_words(uint32_t a0, uint32_t a1, uint32_t sa, uint32_t b0, uint32_t b1, uint32_t sb)
 {
@@ -447,7 +458,7 @@ template <int RAD, bool EDGE, int TAG, int CPL>
 __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, int pitch, int R, int C,
                                                  float* __restrict__ g_out, const Kern& K,
                                                  int x0, int y0, int TH, float* rb, const U8Src& u8,
-                                                 float* __restrict__ nbo)
+                                                 float* __restrict__ nbo, uint32_t* __restrict__ stg)
 {
     // CPL columns per lane (4: 256-column strips, 16-B accesses; 2: 128-column strips,
     // 8-B accesses, half the ring registers -> more waves for the smaller octaves)
@@ -491,6 +502,47 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
     const __amdgpu_buffer_rsrc_t rs_nb =
         __builtin_amdgcn_make_buffer_rsrc(nbo, 0, nbo ? K.nb_rows * K.nb_pitch * 4 : 0, 0x00020000);
 
+    // UP: stage the band's source rows [sr0, sr0 + nrs) -- bytes [s_lo, s_lo + 4 SWD) of each,
+    // from the row's 4-B aligned start (misalignment m of row q: (delta + (sr0+q) ld + s_lo) & 3)
+    // -- into stg[q][SWD] by dword buffer loads (bytes past the image read as 0, no fault)
+    constexpr int SWD = bs_u8_dw(RAD, CPL);
+    const int xs0 = x0 - RH;                               // first upsampled column of the wave's span
+    const int s_lo = max(0, (xs0 >> 1) - 1);               // (>> 1: floor, xs0 may be negative on the left edge)
+    int sr0 = 0;
+    uint32_t delta = 0;
+    if constexpr (UP) {
+        const int p_lo = y0 - RAD - E, p_hi = y0 - RAD - E + F + TH - 1;
+        int ymin = p_lo < 0 ? 0 : p_lo, ymax = p_hi >= R ? R - 1 : p_hi;
+        if (p_lo < 0) ymax = max(ymax, min(-p_lo, R - 1));
+        if (p_hi >= R) ymin = min(ymin, max(2 * R - 2 - p_hi, 0));
+        sr0 = max(0, (ymin >> 1) - 1);
+        const int sr1 = min(u8.rows - 1, (ymax >> 1) + 1);
+        const int total = (sr1 - sr0 + 1) * SWD;           // <= bs_u8_rows(RAD) * SWD (kBaseMaxTH)
+        delta = (uint32_t)(reinterpret_cast<uintptr_t>(u8.p) & 3);
+        const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(u8.p - delta), 0, (int)(delta + (uint32_t)(u8.rows - 1) * (uint32_t)u8.ld + (uint32_t)u8.cols), 0x00020000);
+        constexpr int SCH = 16;                            // loads in flight per lane per round
+        for (int t0 = 0; t0 < total; t0 += 64 * SCH) {
+            uint32_t v[SCH];
+#pragma unroll
+            for (int q = 0; q < SCH; ++q) {
+                const int t = t0 + 64 * q + lane;
+                const int row = t / SWD, k = t - row * SWD;
+                const uint32_t ro = delta + (uint32_t)(sr0 + row) * (uint32_t)u8.ld + (uint32_t)s_lo;
+                v[q] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs_in, t < total ? (ro & ~3u) + 4u * (uint32_t)k : 0x80000000u, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < SCH; ++q)
+                if (t0 + 64 * q + lane < total) stg[t0 + 64 * q + lane] = v[q];
+        }
+        __syncthreads();                                   // one-wave block: LDS writes before the reads
+    }
+    // UP: byte offset of source column x of source row y inside its staged row
+    auto s_off = [&](int y, int x) {
+        return (y - sr0) * (4 * SWD) + (x - s_lo) + (int)((delta + (uint32_t)y * (uint32_t)u8.ld + (uint32_t)s_lo) & 3u);
+    };
+    const uint8_t* const stg8 = reinterpret_cast<const uint8_t*>(stg);
+
     // Prefetch slots.  The DPP layout keeps two sets and alternates them block by block: block
     // parity b consumes set b and refills set 1-b, so a slot's old value is dead before its
     // register is loaded again.  With one set the scheduler hoisted each refill above the last
@@ -523,6 +575,12 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
         else return vo_reflect101(p, R);
     };
     // loads for step kk into prefetch slot SL: input row y0-r-E+kk (reflected)
+    // UP: the word pair of the staged row holding source byte column x (LDS, 4-B aligned)
+    auto s_words = [&](int y, int x) {
+        const int o = s_off(y, x);
+        const uint32_t* w = stg + (o >> 2);
+        return u2_t{w[0], w[1]};
+    };
 #define VO_BS_LOAD(KK, SL)                                                                        \
     do {                                                                                          \
         const int yin_ = yref(KK);                                                                \
@@ -530,16 +588,11 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
             if constexpr (!EDGE) {                                                                \
                 const int ya_ = yin_ >> 1;                                                        \
                 const int yb_ = (yin_ & 1) ? min(ya_ + 1, u8.rows - 1) : max(ya_ - 1, 0);         \
-                const uint8_t* ra_ = u8.p + (size_t)ya_ * u8.ld;                                  \
-                const uint8_t* rb_ = u8.p + (size_t)yb_ * u8.ld;                                  \
-                /* aligned down by pointer arithmetic, not an integer round trip: the pointer */   \
-                /* keeps its global address space, so these are global (in-order) loads, not */    \
-                /* flat ones, which the compiler can only wait for with vmcnt(0) */                 \
-                pw[SL][0] = *reinterpret_cast<const u2_t*>(ra_ + gm - ((uintptr_t)(ra_ + gm) & 3)); \
-                pw[SL][1] = *reinterpret_cast<const u2_t*>(rb_ + gm - ((uintptr_t)(rb_ + gm) & 3)); \
+                pw[SL][0] = s_words(ya_, gm);                                                     \
+                pw[SL][1] = s_words(yb_, gm);                                                     \
                 if constexpr (!XCH) {                                                             \
-                    pw[SL][2] = *reinterpret_cast<const u2_t*>(ra_ + gh - ((uintptr_t)(ra_ + gh) & 3)); \
-                    pw[SL][3] = *reinterpret_cast<const u2_t*>(rb_ + gh - ((uintptr_t)(rb_ + gh) & 3)); \
+                    pw[SL][2] = s_words(ya_, gh);                                                 \
+                    pw[SL][3] = s_words(yb_, gh);                                                 \
                 }                                                                                 \
             }                                                                                     \
         } else {                                                                                  \
@@ -560,21 +613,27 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
         vm = pf[SL];
         if constexpr (!XCH) vh = ph[SL];
         if constexpr (UP) {
-            const int yin = yref(kk);
+            // the prefetch of steps past the band's end read its last row again: same row here
+            const int yin = yref(min(kk, F + TH - 1));
+            const int ya = yin >> 1, yb = (yin & 1) ? min(ya + 1, u8.rows - 1) : max(ya - 1, 0);
             if constexpr (!EDGE) {
-                const int ya = yin >> 1, yb = (yin & 1) ? min(ya + 1, u8.rows - 1) : max(ya - 1, 0);
-                const uintptr_t pb = reinterpret_cast<uintptr_t>(u8.p);   // byte misalignment incl. the image base
-                const uint32_t sa = (uint32_t)((pb + (size_t)ya * u8.ld + gm) & 3), sb = (uint32_t)((pb + (size_t)yb * u8.ld + gm) & 3);
-                vm = up4_from_words(pw[SL][0].x, pw[SL][0].y, sa, pw[SL][1].x, pw[SL][1].y, sb);
-                if constexpr (!XCH) {
-                    const uint32_t ha = (uint32_t)((pb + (size_t)ya * u8.ld + gh) & 3), hb = (uint32_t)((pb + (size_t)yb * u8.ld + gh) & 3);
-                    vh = up4_from_words(pw[SL][2].x, pw[SL][2].y, ha, pw[SL][3].x, pw[SL][3].y, hb);
-                }
-            } else {                                      // border strips: reflected columns, loads in place
+                vm = up4_from_words(pw[SL][0].x, pw[SL][0].y, (uint32_t)s_off(ya, gm) & 3u, pw[SL][1].x, pw[SL][1].y,
+                                    (uint32_t)s_off(yb, gm) & 3u);
+                if constexpr (!XCH)
+                    vh = up4_from_words(pw[SL][2].x, pw[SL][2].y, (uint32_t)s_off(ya, gh) & 3u, pw[SL][3].x, pw[SL][3].y,
+                                        (uint32_t)s_off(yb, gh) & 3u);
+            } else {                                      // border strips: reflected columns, bytes from LDS
+                // up_sample's expressions on the staged bytes
+                auto up_at = [&](int x) {
+                    const int xa = x >> 1, xb = (x & 1) ? (xa + 1 < u8.cols ? xa + 1 : u8.cols - 1) : (xa > 0 ? xa - 1 : 0);
+                    const float ha = 0.75f * (float)stg8[s_off(ya, xa)] + 0.25f * (float)stg8[s_off(ya, xb)];
+                    const float hb = 0.75f * (float)stg8[s_off(yb, xa)] + 0.25f * (float)stg8[s_off(yb, xb)];
+                    return 0.75f * ha + 0.25f * hb;
+                };
 #pragma unroll
                 for (int i = 0; i < CPL; ++i) {
-                    vm[i] = up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, cm[i]);
-                    if constexpr (!XCH) vh[i] = up_sample(u8.p, u8.ld, u8.rows, u8.cols, yin, ch[i]);
+                    vm[i] = up_at(cm[i]);
+                    if constexpr (!XCH) vh[i] = up_at(ch[i]);
                 }
             }
         }
@@ -677,7 +736,7 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
                 // next octave's base (level L; K.nb unset: a zero-size buffer drops it): even rows
                 // -- the even steps u, since y0, F and kk0 - F are multiples of P -- and the lane's
                 // even columns (xl is even)
-                if constexpr ((u & 1) == 0) {
+                if constexpr ((u & 1) == 0 && !(TAG & 1)) {        // (the octave-0 base, TAG & 1, never stores one)
                     const int yn = y >> 1, c0 = xl >> 1;
                     const bool rowok = act && yn < K.nb_rows;
                     const uint32_t nbase = (uint32_t)(yn * K.nb_pitch + c0) * 4u;
@@ -734,6 +793,8 @@ __global__ __launch_bounds__(64, (RAD <= 6 || CPL == 2) ? 3 : 2) void k_blur_str
     constexpr bool XCH = bs_hl(RAD, CPL, TAG);
     // LDS exchange: staged row + per-lane dummy halo slots (unused with the DPP exchange)
     __shared__ __attribute__((aligned(16))) float rb[XCH ? 4 : bs_rw(RAD, CPL) + 64 * CPL];
+    // TAG & 4: the band's staged u8 source rows (10.2 KB at r = 5)
+    __shared__ uint32_t stg[(TAG & 4) ? bs_u8_rows(RAD) * bs_u8_dw(RAD, CPL) : 1];
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int strip = bid % n_strips, tb = bid / n_strips;
     const int band = tb % n_bands, img = tb / n_bands;
@@ -744,17 +805,15 @@ __global__ __launch_bounds__(64, (RAD <= 6 || CPL == 2) ? 3 : 2) void k_blur_str
     const int THb = min(TH, (R - y0 + BS_P - 1) / BS_P * BS_P);
     const size_t os = img * splane, od = img * dplane;
     U8Src u8{nullptr, 0, in_rows, in_cols};
-    int margin = 0;
     if (TAG & 4) {
         u8.p = ((img & 1) ? isrc.right : isrc.left) + (size_t)(img >> 1) * isrc.frame_stride;
         u8.ld = isrc.ld;
-        margin = 16;                                       // 8-B word loads stay inside the source row
     }
     float* const nbo = K.nb ? K.nb + od : nullptr;
-    if (x0 - RH < 0 || (XCH ? x0 - RH + 64 * CPL : x0 + SW + RH) + margin > C)
-        blur_stream_body<RAD, true, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, THb, rb, u8, nbo);
+    if (x0 - RH < 0 || (XCH ? x0 - RH + 64 * CPL : x0 + SW + RH) > C)
+        blur_stream_body<RAD, true, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, THb, rb, u8, nbo, stg);
     else
-        blur_stream_body<RAD, false, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, THb, rb, u8, nbo);
+        blur_stream_body<RAD, false, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, THb, rb, u8, nbo, stg);
 }
 
 // next octave base: G0 of octave o = G_L of octave o-1 decimated by 2.  Grid (column blocks of
@@ -1354,6 +1413,10 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
     __shared__ __attribute__((aligned(16))) uint32_t hp[HS * NC];
     __shared__ float tf[VO_SIFT_ORI_BINS];
     __shared__ float hs[VO_SIFT_ORI_BINS];
+    // separable window weights (vo_spec.h vo_sift_wt) for radii up to OWT; larger windows (sigma
+    // far above the default) evaluate the same factors inline -- the same bits either way
+    constexpr int OWT = 64;
+    __shared__ float wtab[OWT + 1];
     const int lane = threadIdx.x;
     __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
     const long total = flat_setup(n_cand, cand_cap, n_img, fpre);
@@ -1372,6 +1435,9 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
         const int radius = vo_round(VO_SIFT_ORI_RADIUS * scl);
         const float sigw = VO_SIFT_ORI_SIG * scl;
         const float expf_scale = -1.0f / (2.0f * sigw * sigw);
+        const bool tab = radius <= OWT;                    // wave-uniform
+        if (tab)
+            for (int k2 = lane; k2 <= radius; k2 += 64) wtab[k2] = vo_sift_wt(expf_scale, k2);
         typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int b2 = 4 * lane; b2 < HS * NC; b2 += 256) *reinterpret_cast<u4_t*>(&hp[b2]) = u4_t{0u, 0u, 0u, 0u};
@@ -1407,8 +1473,8 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
 #pragma unroll
             for (int q = 0; q < U; ++q) {
                 const float dx = gx[q], dy = gy[q];
-                const float fi = (float)ii[q], fj = (float)jj[q];            // i^2 + j^2 exact in float
-                float w = vo_expf_nonpos((fi * fi + fj * fj) * expf_scale);   // arg in [-21, 0]
+                const int ai = abs(ii[q]), aj = abs(jj[q]);
+                const float w = tab ? wtab[ai] * wtab[aj] : vo_sift_wt(expf_scale, ai) * vo_sift_wt(expf_scale, aj);
                 float mag = vo_grad_mag(dx, dy);
                 float ori = vo_atan2_deg(dy, dx);
                 int bin = vo_round((float)VO_SIFT_ORI_BINS / 360.0f * ori);   // ori in [0, 360): bin in [0, 36]
@@ -1535,28 +1601,14 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
 // u32 fixed point (vo_desc_fx_quant) sums are order-free, so the copies are folded after
 // the loop without changing a bit.
 #define DCS 324
-// paired layout (VO_DESC_PAIR): (DW+2)^2 cells x DN u64 slots = 288, stride 290 u64 (= 4 mod 64 banks)
-#define DCS2 290
-#ifndef VO_DESC_PAIR
-#define VO_DESC_PAIR 0
-#endif
 #ifndef VO_DESC_COPIES
 #define VO_DESC_COPIES 4
 #endif
 #ifndef VO_DESC_WAVES
 #define VO_DESC_WAVES 5           // waves per SIMD the register budget is sized for (96 VGPRs)
 #endif
-#ifndef VO_DESC_LOOP
-#define VO_DESC_LOOP 1            // 1: block row lookup + pipelined gradient loads; 0: per-lane row walk
-#endif
 #ifndef VO_DESC_U
-#define VO_DESC_U 2               // blocks of 64 samples per batch (VO_DESC_LOOP 1)
-#endif
-#ifndef VO_DESC_MARGIN
-#define VO_DESC_MARGIN 0          // extra columns around the descriptor rows' real-arithmetic bounds
-#endif
-#ifndef VO_DESC_ADDR
-#define VO_DESC_ADDR 1            // 1: buffer gradient loads from one 32-bit offset, 24-bit index multiplies
+#define VO_DESC_U 2               // blocks of 64 samples per batch
 #endif
 template <int DCOPIES>
 __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
@@ -1564,19 +1616,17 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
                                              uint8_t* __restrict__ desc, DescMeta* __restrict__ meta, int kp_cap, int n_img)
 {
     static_assert(DCS >= DHIST, "copy stride holds a histogram");
-#if VO_DESC_PAIR
-    // bin pairs: slot (cell, o) is a u64 whose low word sums bin o and high word bin o+1 (mod DN)
-    // of that cell, so one 64-bit LDS add carries both orientation neighbours of a sample
-    __shared__ uint64_t hfx2[DCOPIES * DCS2];
-    uint32_t* const hfx = reinterpret_cast<uint32_t*>(hfx2);
-#else
     __shared__ __attribute__((aligned(16))) uint32_t hfx[DCOPIES * DCS];
-#endif
     // One packed entry per window row r: (index of the row's first sample) | (its first column j,
     // int16) << 16; entry nrows is the sample count, entries nrows+1 .. nrows+8 a 0xFFFF sentinel
-    // start.  Starts fit 16 bits: the window holds <= 2 r^2 + O(r) samples (< 34k at r = RMAX).
-    // 7.3 KB of LDS with the histograms -> 5 one-wave workgroups per SIMD.
+    // start.  Starts fit 16 bits: a window never holds more than its (2 r + 1)^2 square, which
+    // the cap r <= VO_SIFT_DESCR_RMAX = 127 bounds by 65025 (the rotated square alone is
+    // ~2 r^2 + O(r) samples, but a capped radius can leave the whole square inside it).
+    // 7.8 KB of LDS with the histograms and weights -> 5 one-wave workgroups per SIMD.
+    static_assert((2 * VO_SIFT_DESCR_RMAX + 1) * (2 * VO_SIFT_DESCR_RMAX + 1) <= 0xFFFF, "16-bit row starts");
     __shared__ uint32_t rtab[2 * VO_SIFT_DESCR_RMAX + 2 + 8];
+    // separable window weights (vo_spec.h vo_sift_wt): w(i, j) = wtab[|i|] * wtab[|j|]; 0.5 KB
+    __shared__ float wtab[VO_SIFT_DESCR_RMAX + 1];
     const int lane = threadIdx.x;
     __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
     const long total = flat_setup(n_kp, kp_cap, n_img, fpre);
@@ -1589,13 +1639,9 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
         const OctGeom& g = py->oct[q.o];
         const int rows = g.rows, cols = g.cols, P = g.pitch;
         const float* gim = arena + g.g_off[q.layer] + img * py->istride;
-#if VO_DESC_PAIR
-        for (int b = lane; b < DCOPIES * DCS2; b += 64) hfx2[b] = 0ull;
-#else
         static_assert((DCOPIES * DCS) % 4 == 0, "16-B zeroing");
         typedef uint32_t u4z_t __attribute__((ext_vector_type(4)));
         for (int b = 4 * lane; b < DCOPIES * DCS; b += 256) *reinterpret_cast<u4z_t*>(&hfx[b]) = u4z_t{0u, 0u, 0u, 0u};
-#endif
         float ori = 360.0f - q.angle;
         if (fabsf(ori - 360.0f) < VO_FLT_EPSILON) ori = 0.0f;
         const int px = vo_round(q.xo), pyy = vo_round(q.yo);
@@ -1609,6 +1655,10 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
         if (radius > VO_SIFT_DESCR_RMAX) radius = VO_SIFT_DESCR_RMAX;
         cos_t = cos_t / hist_width;
         sin_t = sin_t / hist_width;
+        {
+            const float wsc = exp_scale / (hist_width * hist_width);
+            for (int k2 = lane; k2 <= radius; k2 += 64) wtab[k2] = vo_sift_wt(wsc, k2);
+        }
         // Only ~half of the (2r+1)^2 window lies inside the rotated 4x4-cell square.  Each
         // window row i gets a conservative column interval [jlo, jhi] (a superset: +-2
         // columns of margin over the real-arithmetic bounds, clamped to the image
@@ -1625,19 +1675,19 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
                 // |j*ct - i*st| < lim  and  |j*st + i*ct| < lim  (rbin = r_rot + 1.5 in (-1, DW)); lim is
                 // 1e-3 bin widths wider than the test below, far above the float error of the test
                 // (~1e-6) and of these bounds (< 1e-4 columns at r <= RMAX), so [floor(a), ceil(b)]
-                // holds every accepted column (VO_DESC_MARGIN extra columns of margin)
+                // holds every accepted column
                 const float fi = (float)i, lim = 0.5f * DW + 0.5f + 1e-3f, cap = (float)(radius + 2);
                 if (fabsf(cos_t) > 1e-9f) {
                     float a = (fi * sin_t - lim) * inv_ct, b = (fi * sin_t + lim) * inv_ct;
                     if (a > b) { const float t2 = a; a = b; b = t2; }
                     a = fminf(fmaxf(a, -cap), cap); b = fminf(fmaxf(b, -cap), cap);
-                    jlo = max(jlo, (int)floorf(a) - VO_DESC_MARGIN); jhi = min(jhi, (int)ceilf(b) + VO_DESC_MARGIN);
+                    jlo = max(jlo, (int)floorf(a)); jhi = min(jhi, (int)ceilf(b));
                 } else if (fabsf(fi * sin_t) >= lim) { jlo = 1; jhi = 0; }
                 if (fabsf(sin_t) > 1e-9f) {
                     float a = (-fi * cos_t - lim) * inv_st, b = (-fi * cos_t + lim) * inv_st;
                     if (a > b) { const float t2 = a; a = b; b = t2; }
                     a = fminf(fmaxf(a, -cap), cap); b = fminf(fmaxf(b, -cap), cap);
-                    jlo = max(jlo, (int)floorf(a) - VO_DESC_MARGIN); jhi = min(jhi, (int)ceilf(b) + VO_DESC_MARGIN);
+                    jlo = max(jlo, (int)floorf(a)); jhi = min(jhi, (int)ceilf(b));
                 } else if (fabsf(fi * cos_t) >= lim) { jlo = 1; jhi = 0; }
                 jlo = max(jlo, 1 - px); jhi = min(jhi, cols - 2 - px);
                 // trim the superset to the exact set: the float test below is monotone
@@ -1677,33 +1727,14 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
             if (lane < 8) rtab[nrows + 1 + lane] = 0xFFFFu;
         }
         __syncthreads();
-#if VO_DESC_DIAG_NOLOOP
-        const int nsamp = 0 * (int)rtab[nrows];   // timing diagnostic only: per-keypoint work without samples
-#else
         const int nsamp = (int)rtab[nrows];
-#endif
-#if VO_DESC_PAIR
-        uint64_t* hc2 = hfx2 + (lane & (DCOPIES - 1)) * DCS2;
-#else
         uint32_t* hc = hfx + (lane & (DCOPIES - 1)) * DCS;
-#endif
-#if VO_DESC_DIAG_NOATOMIC
-        uint32_t diag = 0;
-#endif
         // one sample: weights, bins, fixed-point LDS atomics
-        auto accum = [&](float c_rot, float r_rot, float dx, float dy) {
+        auto accum = [&](float c_rot, float r_rot, float w, float dx, float dy) {
             float rbin = r_rot + (float)(DW / 2) - 0.5f;
             float cbin = c_rot + (float)(DW / 2) - 0.5f;
-#if VO_DESC_DIAG_NOMATH
-            // timing diagnostic only (not bit-exact): exp, atan2 and sqrt replaced by cheap terms
-            float w = 1.0f + (c_rot * c_rot + r_rot * r_rot) * exp_scale;
-            float ang = fminf(fabsf(dy) * 57.0f + fabsf(dx), 359.0f);
-            float mag = ((fabsf(dx) + fabsf(dy)) * w) * VO_DESC_FX_SCALE;
-#else
-            float w = vo_expf_nonpos((c_rot * c_rot + r_rot * r_rot) * exp_scale);   // listed samples: arg in (-1.6, 0]
             float ang = vo_atan2_deg(dy, dx);
             float mag = (vo_grad_mag(dx, dy) * w) * VO_DESC_FX_SCALE;
-#endif
             float obin = (ang - ori) * bins_per_deg;
             // floors kept in float ((float)(int)floorf(v) == floorf(v) here); the cell index is an
             // exact small-integer float expression, one conversion; obin in [-8, 8] so the circular
@@ -1719,22 +1750,6 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
             float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
             float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
             float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-#if VO_DESC_PAIR
-            uint64_t* h = hc2 + cell * DN + o0;
-            auto pk = [](float lo, float hi) {
-                return (unsigned long long)vo_desc_fx_quant(lo) | ((unsigned long long)vo_desc_fx_quant(hi) << 32);
-            };
-            atomicAdd((unsigned long long*)h, pk(v_rco000, v_rco001));
-            atomicAdd((unsigned long long*)(h + DN), pk(v_rco010, v_rco011));
-            atomicAdd((unsigned long long*)(h + (DW + 2) * DN), pk(v_rco100, v_rco101));
-            atomicAdd((unsigned long long*)(h + (DW + 3) * DN), pk(v_rco110, v_rco111));
-#elif VO_DESC_DIAG_NOATOMIC
-            // timing diagnostic only (not bit-exact): the sample's 8 contributions summed in place
-            uint32_t* h = hc + cell * DBS + o0;
-            diag += vo_desc_fx_quant(v_rco000) + vo_desc_fx_quant(v_rco001) + vo_desc_fx_quant(v_rco010) +
-                    vo_desc_fx_quant(v_rco011) + vo_desc_fx_quant(v_rco100) + vo_desc_fx_quant(v_rco101) +
-                    vo_desc_fx_quant(v_rco110) + vo_desc_fx_quant(v_rco111) + (uint32_t)(size_t)h;
-#else
             uint32_t* h = hc + (int)((float)cell * (float)DBS) + o0;     // exact: < 2^24
             atomicAdd(h, vo_desc_fx_quant(v_rco000));
             atomicAdd(h + 1, vo_desc_fx_quant(v_rco001));
@@ -1744,67 +1759,24 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
             atomicAdd(h + (DW + 2) * DBS + 1, vo_desc_fx_quant(v_rco101));
             atomicAdd(h + (DW + 3) * DBS, vo_desc_fx_quant(v_rco110));
             atomicAdd(h + (DW + 3) * DBS + 1, vo_desc_fx_quant(v_rco111));
-#endif
         };
         // the gradient neighbours of a listed sample (every listed sample is interior): x+1, x-1 as
         // one 12-B load (through a 3-float type declared with the 4-B alignment the address has),
         // y-1, y+1
-#if VO_DESC_ADDR
         // buffer loads with one 32-bit lane offset: the resource starts at the sample's row y-1
         // column x-1 for offset 0 (gim - P - 1), so row y-1 is +4 B, row y (x-1..x+1) +4P B and
         // row y+1 +8P + 4 B -- no 64-bit address arithmetic per sample; the row offset is a
         // 24-bit multiply (|i| <= RMAX, P < 2^23)
         const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)(gim - P - 1), 0, 0x7FFFFFF0, 0x00020000);
         const int c_off = pyy * P + px;                  // wave-uniform
-#endif
         auto grad_loads = [&](int i, int j, float* g4) {
-#if VO_DESC_DIAG_NOLOAD
-            // timing diagnostic only (not bit-exact): gradients synthesised, no loads
-            g4[0] = (float)(i * 3 + j); g4[1] = (float)(j * 5 - i); g4[2] = (float)(i ^ j); g4[3] = (float)(i - 2 * j);
-#elif VO_DESC_ADDR
             const int vo = 4 * (c_off + __mul24(i, P) + j);
             typedef int i3_t __attribute__((ext_vector_type(3)));
             const i3_t h = __builtin_amdgcn_raw_buffer_load_b96(grs, vo, 4 * P, 0);
             g4[0] = __int_as_float(h.z); g4[1] = __int_as_float(h.x);
             g4[2] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 0, 0));
             g4[3] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 8 * P, 0));
-#else
-            typedef float f3u_t __attribute__((ext_vector_type(3), aligned(4)));
-            const float* gp = gim + (uint32_t)((pyy + i) * P + px + j);   // 32-bit offset from the uniform base
-            const f3u_t h = *reinterpret_cast<const f3u_t*>(gp - 1);
-            g4[0] = h.z; g4[1] = h.x;
-            g4[2] = gp[-(ptrdiff_t)P]; g4[3] = gp[P];
-#endif
         };
-#if VO_DESC_LOOP == 0
-        {   // per-lane walk over the row table
-            int lo = 0;                                      // current row; s only grows, so advance
-            constexpr int U = 4;                             // samples per lane per iteration: 16 loads in flight
-            for (int s0 = lane; s0 < nsamp; s0 += 64 * U) {
-                int ii[U], jj[U];
-                bool ok[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int s = s0 + 64 * u;
-                    ok[u] = s < nsamp;
-                    const int sc = ok[u] ? s : nsamp - 1;
-                    while ((int)(rtab[lo + 1] & 0xFFFFu) <= sc) ++lo;
-                    const uint32_t e = rtab[lo];
-                    ii[u] = lo - radius; jj[u] = ((int)e >> 16) + (sc - (int)(e & 0xFFFFu));
-                }
-                float g4[U][4];
-#pragma unroll
-                for (int u = 0; u < U; ++u) grad_loads(ii[u], jj[u], g4[u]);
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (ok[u]) {
-                        const float fi = (float)ii[u], fj = (float)jj[u];
-                        accum(fj * cos_t - fi * sin_t, fj * sin_t + fi * cos_t, g4[u][0] - g4[u][1], g4[u][2] - g4[u][3]);
-                    }
-                }
-            }
-        }
-#else
         {   // Block lookup: the 64 samples bs .. bs+63 of a block start in row rb (wave-uniform) and
             // span a few rows; every lane reads the same K+2 table entries (LDS broadcast, one round
             // trip) and selects its row by comparing its sample index with the row starts -- no
@@ -1850,7 +1822,8 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
                 for (int u = 0; u < U; ++u) {
                     if (sb + 64 * u + lane < nsamp) {
                         const float fi = (float)S[u].i, fj = (float)S[u].j;
-                        accum(fj * cos_t - fi * sin_t, fj * sin_t + fi * cos_t, S[u].g[0] - S[u].g[1], S[u].g[2] - S[u].g[3]);
+                        accum(fj * cos_t - fi * sin_t, fj * sin_t + fi * cos_t, wtab[abs(S[u].i)] * wtab[abs(S[u].j)],
+                              S[u].g[0] - S[u].g[1], S[u].g[2] - S[u].g[3]);
                     }
                 }
             };
@@ -1870,7 +1843,6 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
                 }
             }
         }
-#endif
         __syncthreads();
         // fold the circular orientation bins and convert; lane holds dst[lane], dst[lane+64]
         float dv[2];
@@ -1881,24 +1853,11 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
             const int ci = cell / DW, cj = cell - ci * DW;
             const int base = ((ci + 1) * (DW + 2) + (cj + 1)) * DBS;
             uint32_t v = 0;
-#if VO_DESC_PAIR
-            const int cbase = ((ci + 1) * (DW + 2) + (cj + 1)) * DN;
-#pragma unroll
-            for (int cp = 0; cp < DCOPIES; ++cp) {
-                v += hfx[2 * (cp * DCS2 + cbase + ob)];                              // low word: bin ob
-                v += hfx[2 * (cp * DCS2 + cbase + ((ob + DN - 1) & (DN - 1))) + 1];  // high word of ob-1
-            }
-            (void)base;
-#else
 #pragma unroll
             for (int cp = 0; cp < DCOPIES; ++cp) {
                 v += hfx[cp * DCS + base + ob];
                 if (ob == 0) v += hfx[cp * DCS + base + DN];
             }
-#endif
-#if VO_DESC_DIAG_NOATOMIC
-            v += diag & 1u;
-#endif
             dv[h] = vo_desc_fx_to_float(v);
         }
         float s = dv[0] * dv[0] + dv[1] * dv[1];
@@ -1988,6 +1947,7 @@ static bool launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
         const int cpl = (!base && C <= kCpl2MaxC) ? 2 : 4;
         const int n_strips = (C + 64 * cpl - 1) / (64 * cpl);
         const long rows_total = (long)R * n_strips * grid.z;
+        static_assert(kMaxTH <= kBaseMaxTH, "the staged octave-0 base stages at most kBaseMaxTH-row bands");
         int TH = (int)std::min<long>(kMaxTH, rows_total / kWaveTarget);
         TH = std::max(BS_P, TH / BS_P * BS_P);
         if (R >= TH && R > RAD + BS_P + 2) {             // (one reflection fold per band edge)
@@ -2035,16 +1995,21 @@ static float ext_threshold(const Pyramid& py, const vo_sift_params& p)
 }
 
 // octaves [0, n) whose levels 1..L+2, extremum test and next base k_octave computes in one pass
-// (octave.hip): a prefix of the octaves, below the LDS-sized ones.  Experimental and OFF unless the
-// environment sets VO_FUSED_OCTAVE=1: bit-exact, but measured 2.4x slower than the per-level
-// kernels on MI355X -- read at every enqueue so one process can test both paths.
+// (octave.hip): a prefix of the octaves, below the LDS-sized ones.  Experimental: bit-exact but
+// measured 2.4x slower than the per-level kernels on MI355X, so it is compiled only
+// into the test build libvo_exp.so (VO_EXPERIMENTAL, selected there by vo_exp_set); the product
+// library always takes the per-level kernels.
 static int fused_octaves(const Pyramid& py)
 {
-    const char* e = getenv("VO_FUSED_OCTAVE");
-    if (!e || e[0] != '1') return 0;
+#if VO_EXPERIMENTAL
+    if (!g_exp_fused_octave) return 0;
     int n = 0;
     while (n < py.n_oct && octave_fused_ok(py, n)) ++n;
     return n;
+#else
+    (void)py;
+    return 0;
+#endif
 }
 
 // First octave from which every remaining octave fits the one-launch LDS path (k_small_pyr),
@@ -2070,10 +2035,10 @@ static SmallPlan small_plan(const Pyramid& py)
     return sp;
 }
 
-// The LDS-sized octaves (one k_small_pyr launch).  Enqueued at the head of the feature stages,
-// not at the tail of the scale space: each of its workgroups needs ~120 KB of one CU's LDS, which
-// the scale-space stream only finds once the previous batch's descriptor waves (6.7 KB each, up
-// to 20 per CU) have drained -- at the head of the feature stream they have, by stream order.
+// The LDS-sized octaves (one k_small_pyr launch).  sift_enqueue_pyramid_tail enqueues it on the
+// scale-space stream after the last level blur (its workgroups need ~120 KB of one CU's LDS; by
+// then octave 0's extremum test has moved to the feature stream, so the previous batch's
+// descriptor waves no longer hold every CU's LDS when it arrives -- DESIGN.md §9c).
 static void sift_enqueue_small(const Pyramid& py, SiftBuffers& b, int n_img, hipStream_t s, const Pyramid* d_py)
 {
     const SmallPlan sp = small_plan(py);
@@ -2098,7 +2063,9 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
         hipMemset2DAsync(b.mask + w0, sizeof(unsigned long long) * py.n_words, 0, sizeof(unsigned long long) * (w1 - w0),
                          n_img, s);
     }
+#if VO_EXPERIMENTAL
     const float thr = ext_threshold(py, p);
+#endif
     bool base_done = false;                            // octave o's base already stored
     for (int o = 0; o < py.n_oct; ++o) {
         const OctGeom& g = py.oct[o];
@@ -2130,10 +2097,12 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
                       A + g.g_off[0], py.istride, g.pitch, C);
         }
         base_done = false;
+#if VO_EXPERIMENTAL
         if (o < n_fused) {
             octave_fused_launch(py, d_py, b, o, n_img, thr, s);
             continue;
         }
+#endif
         for (int i = 1; i < L + 3; ++i) {
             Kern K = make_kern(py, i);
             // level L stores the next octave's base from its store path (no k_down pass: that
@@ -2159,9 +2128,9 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
 // often enough for the scale-space stream's blurs to get slots while they run
 constexpr int kFeatureGrid = 32768;
 
-// The extremum test runs at the head of the feature stages, not at the tail of the scale
-// space: the scale-space stream is the pipeline's critical path (7.1 of 7.9 ms per 64-frame
-// step in situ, against 4.7 ms of feature stages), so the test's 1.7 ms balance the streams.
+// The extremum test of octaves [o_begin, o_end).  vo_api.hip enqueues it in two parts on the
+// feature stream: octave 0 as soon as the scale-space stream records ev_o0 (beside the level blurs
+// of octaves 1..), and octaves 1.. after the scale space's tail (VO_EXT_SPLIT).
 void sift_enqueue_extrema(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
                           const Pyramid* d_py, int o_begin, int o_end)
 {

@@ -1246,3 +1246,20 @@ int vo_landmarks(vo_ctx* c, const float* l_pos, const float* r_pos, int S, const
 }
 
 }  // extern "C"
+
+#if VO_EXPERIMENTAL
+// ---------------------------------------------------------------------------
+// Test build only (libvo_exp.so, make exp): selects the experimental kernels that the product
+// library does not contain -- the fused octave (octave.hip) and the eager MSAC kernels -- so
+// their parity tests can run them against the default path.  Process-wide; read at enqueue.
+// ---------------------------------------------------------------------------
+namespace vo {
+int g_exp_fused_octave = 0, g_exp_msac_eager = 0;
+}
+extern "C" int vo_exp_set(int fused_octave, int msac_eager)
+{
+    vo::g_exp_fused_octave = fused_octave ? 1 : 0;
+    vo::g_exp_msac_eager = msac_eager ? 1 : 0;
+    return VO_OK;
+}
+#endif

@@ -180,9 +180,14 @@ struct OctArgs {
     float k[6][16];                     // taps of levels 1..5 (k[i][0..r_i])
     int n_strips, pad2;
 };
+#if VO_EXPERIMENTAL
+// test build only (libvo_exp.so): the fused octave (octave.hip) and the eager MSAC kernels, each
+// selected by vo_exp_set; the product libvo.so has neither the kernels nor a switch
 bool octave_fused_ok(const Pyramid& py, int o);
 void octave_fused_launch(const Pyramid& py, const Pyramid* d_py, const SiftBuffers& b, int o, int n_img, float thr,
                          hipStream_t s);
+extern int g_exp_fused_octave, g_exp_msac_eager;
+#endif
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize, 160 KB) once per (kernel, device)
 void raise_lds_limit(const void* fn);
 

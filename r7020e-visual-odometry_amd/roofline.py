@@ -13,7 +13,6 @@ bytes per launch / average launch duration of the dominant kernel.
 from __future__ import annotations
 
 import math
-import os
 
 SMALL_PX = 9216   # csrc/sift.hip VO_SMALL_PX
 
@@ -40,12 +39,10 @@ def pyramid_bytes_per_image(rows: int, cols: int, layers: int = 3) -> int:
 FUSED_MIN_COLS, FUSED_MIN_ROWS = 256, 64   # csrc/octave.hip octave_fused_ok (default SIFT radii, 3 layers)
 
 
-def fused_octaves(rows: int, cols: int, layers: int = 3, enabled: bool | None = None) -> int:
-    """Octaves [0, n) libvo builds with k_octave (levels 1..L+2, extremum test and the next
-    base in one pass): the leading octaves at least 256 columns wide and 64 rows tall -- only
-    when the experimental path is on (VO_FUSED_OCTAVE=1, as csrc/sift.hip fused_octaves reads)."""
-    if enabled is None:
-        enabled = os.environ.get("VO_FUSED_OCTAVE", "0").startswith("1")
+def fused_octaves(rows: int, cols: int, layers: int = 3, enabled: bool = False) -> int:
+    """Octaves [0, n) the test build libvo_exp.so builds with k_octave when vo_exp_set selects it
+    (levels 1..L+2, extremum test and the next base in one pass): the leading octaves at least
+    256 columns wide and 64 rows tall.  The product libvo.so has no k_octave: 0 by default."""
     if layers != 3 or not enabled:
         return 0
     dims = octave_dims(rows, cols)
@@ -56,7 +53,7 @@ def fused_octaves(rows: int, cols: int, layers: int = 3, enabled: bool | None = 
     return n
 
 
-def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3, fused: bool | None = None) -> dict:
+def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3, fused: bool = False) -> dict:
     """Algorithmic bytes per CALL (all launches of that kernel name in one
     batch of n_img images) and launches per call, per kernel name."""
     dims = octave_dims(rows, cols)

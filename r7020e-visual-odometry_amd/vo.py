@@ -95,15 +95,21 @@ EXPORTS = [
     "vo_sift_ex", "vo_step_batch_ex", "vo_chain_poses", "vo_landmarks_to_world_frames",
 ]
 
-_lib = None
+# the test build (csrc `make exp`, -DVO_EXPERIMENTAL=1): libvo plus the experimental kernels kept
+# as cross-checks (fused octave, eager MSAC), selected by its extra export vo_exp_set.  Only the
+# parity tests load it (load_experimental_library); the product path never does.
+EXP_LIBPATH = PKG / "lib" / "libvo_exp.so"
+
+_libs: dict = {}
 
 
 def load_library(path: str | os.PathLike | None = None):
-    """Load libvo.so (built in-tree by __graft_entry__.build()).  Raises if absent."""
-    global _lib
-    if _lib is not None:
-        return _lib
+    """Load libvo.so (built in-tree by __graft_entry__.build()).  Raises if absent.  One handle
+    per path (the default path, or $VO_LIBPATH, unless `path` is given)."""
     p = Path(path) if path else Path(os.environ.get("VO_LIBPATH", LIBPATH))
+    key = str(p.resolve()) if p.exists() else str(p)
+    if key in _libs:
+        return _libs[key]
     if not p.exists():
         raise VOError(VO_ERR_STATE, f"{p} not built; run __graft_entry__.build() (make -C csrc)")
     # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same
@@ -167,7 +173,17 @@ def load_library(path: str | os.PathLike | None = None):
                                                P(C.c_double)]
     L.vo_chain_poses.argtypes = [P(C.c_double), P(C.c_int32), C.c_int, P(C.c_double), P(C.c_double)]
     L.vo_kernel_times.argtypes = [vp, P(C.c_char_p), P(C.c_double), P(C.c_int), C.c_int, P(C.c_int)]
-    _lib = L
+    _libs[key] = L
+    return L
+
+
+def load_experimental_library():
+    """The test build libvo_exp.so (see EXP_LIBPATH) with `vo_exp_set(fused_octave, msac_eager)`
+    bound; pass it to Context(lib=...)."""
+    L = load_library(EXP_LIBPATH)
+    if not hasattr(L, "vo_exp_set"):
+        raise VOError(VO_ERR_STATE, f"{EXP_LIBPATH} lacks vo_exp_set (not a VO_EXPERIMENTAL build)")
+    L.vo_exp_set.argtypes = [C.c_int, C.c_int]
     return L
 
 
@@ -207,8 +223,9 @@ class Context:
     """One libvo context (one HIP device, fixed image size, up to max_batch frames per call)."""
 
     def __init__(self, rows: int = 375, cols: int = 1242, max_batch: int = 1, device: int = 0, calib: Calib | None = None,
-                 sift: SiftParams | None = None, match: MatchParams | None = None, ransac: RansacParams | None = None):
-        self.lib = load_library()
+                 sift: SiftParams | None = None, match: MatchParams | None = None, ransac: RansacParams | None = None,
+                 lib=None):
+        self.lib = lib if lib is not None else load_library()
         self.rows, self.cols, self.max_batch = rows, cols, max_batch
         self.sift_params = sift or default_sift_params()
         self.match_params = match or default_match_params()

@@ -49,6 +49,26 @@ def test_product_never_imports_or_links_the_oracle():
     assert "oracle" not in out
 
 
+def test_product_library_has_no_experiments_or_env_switches():
+    """The experimental kernels (fused octave, eager MSAC) live only in the test build
+    libvo_exp.so (csrc `make exp`, -DVO_EXPERIMENTAL=1); the product library carries neither the
+    kernels nor any environment-variable switch."""
+    lib = PKG / "lib" / "libvo.so"
+    syms = subprocess.run(["nm", "-C", str(lib)], capture_output=True, text=True, check=True).stdout
+    for k in ("k_octave", "k_msac_hyp", "k_msac_score", "k_msac_select", "vo_exp_set"):
+        assert k not in syms, k
+    dyn = subprocess.run(["nm", "-D", "--undefined-only", str(lib)], capture_output=True, text=True, check=True).stdout
+    assert "getenv" not in dyn
+    for src in (PKG / "csrc").glob("*.hip"):
+        for ln in src.read_text().splitlines():
+            assert "getenv(" not in ln, (src.name, ln)
+    exp = PKG / "lib" / "libvo_exp.so"
+    assert exp.exists(), "build() builds the test build too"
+    xs = subprocess.run(["nm", "-C", str(exp)], capture_output=True, text=True, check=True).stdout
+    for k in ("k_octave", "k_msac_hyp", "vo_exp_set"):
+        assert k in xs, k
+
+
 def test_no_gpu_means_loud_failure(vo):
     import torch
     if torch.cuda.is_available():
@@ -57,8 +77,7 @@ def test_no_gpu_means_loud_failure(vo):
         vo.Context(375, 1242, 1)
 
 
-def test_missing_library_raises(vo, tmp_path, monkeypatch):
-    monkeypatch.setattr(vo, "_lib", None)
+def test_missing_library_raises(vo, tmp_path):
     with pytest.raises(vo.VOError):
         vo.load_library(tmp_path / "nope.so")
 

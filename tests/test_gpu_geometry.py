@@ -79,22 +79,30 @@ def test_estworldpose_bit_exact(vo, oracle, seed):
 
 
 @pytest.mark.parametrize("outlier_frac,max_trials", [(0.6, 1000), (0.75, 2048), (0.2, 10), (0.5, 100), (0.9, 130)])
-def test_estworldpose_lazy_chunks_equal_oracle_and_eager(vo, oracle, outlier_frac, max_trials, monkeypatch):
+def test_estworldpose_lazy_chunks_equal_oracle_and_eager(vo, oracle, outlier_frac, max_trials):
     """k_msac walks the slots in chunks of 64 and stops at the chunk where the adaptive replay
     stops: at high outlier ratios the replay runs over several chunks (or all of them), at
     small MaxNumTrials the last chunk is partial.  Results equal the oracle's sequential MSAC
-    and the eager kernels (VO_MSAC_EAGER=1: every slot generated and scored) bit for bit."""
+    and the eager kernels (every slot generated and scored; compiled only into the test build
+    libvo_exp.so, selected by vo_exp_set) bit for bit."""
     rng = np.random.default_rng(int(outlier_frac * 100) + max_trials)
     uv, Xw, K = _pose_problem(rng, n=500, outlier_frac=outlier_frac)
     rp = vo.default_ransac_params()
     rp.max_num_trials = max_trials
     orp = oracle.ransac_params()
     orp.max_num_trials = max_trials
-    ctx = vo.Context(375, 1242, 1, ransac=rp)
     ref = oracle.estworldpose(uv, Xw, K, params=orp, frame_key=7)
-    for eager in ("0", "1"):
-        monkeypatch.setenv("VO_MSAC_EAGER", eager)
-        st, T, inl, nin = ctx.estworldpose(uv, Xw, K, params=rp, frame_key=7, raise_on_failure=False)
+    exp = vo.load_experimental_library()
+    for eager, lib in ((0, None), (1, exp)):
+        ctx = vo.Context(375, 1242, 1, ransac=rp, lib=lib)
+        if lib is not None:
+            lib.vo_exp_set(0, 1)
+        try:
+            st, T, inl, nin = ctx.estworldpose(uv, Xw, K, params=rp, frame_key=7, raise_on_failure=False)
+        finally:
+            if lib is not None:
+                lib.vo_exp_set(0, 0)
+            ctx.close()
         assert st == ref[0], (eager, st, ref[0])
         if st == 0:
             assert np.array_equal(T, ref[1]) and np.array_equal(inl, ref[2]) and nin == ref[3]

@@ -50,10 +50,11 @@ def test_gaussian_levels_bit_exact(vo, oracle, syn, shape):
 
 
 @pytest.mark.parametrize("shape", [(375, 1242), (400, 1800), (240, 700)])
-def test_experimental_fused_octave_path_equals_default(vo, oracle, syn, shape, monkeypatch):
-    """The experimental k_octave path (octave.hip, VO_FUSED_OCTAVE=1: levels 1..5, extremum test
-    and next base of each large octave in one launch) gives the same Gaussian planes, keypoints,
-    descriptors and stereo pairs as the default per-level kernels, bit for bit."""
+def test_experimental_fused_octave_path_equals_default(vo, oracle, syn, shape):
+    """The experimental k_octave path (octave.hip, compiled only into the test build
+    libvo_exp.so and selected there by vo_exp_set: levels 1..5, extremum test and next base of
+    each large octave in one launch) gives the same Gaussian planes, keypoints, descriptors and
+    stereo pairs as the product libvo.so's per-level kernels, bit for bit."""
     import torch
     rows, cols = shape
     B = 2
@@ -63,16 +64,22 @@ def test_experimental_fused_octave_path_equals_default(vo, oracle, syn, shape, m
         L[f], R[f] = syn.stereo_pair(syn.SEED_BASE + 310 + f, rows, cols)
     dl, dr = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
     torch.cuda.synchronize()
+    exp = vo.load_experimental_library()
     outs = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("VO_FUSED_OCTAVE", flag)
-        ctx = vo.Context(rows, cols, B)
-        ctx.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), B)
-        planes = [ctx.fetch_gaussian(img, o, i) for img in (0, 3) for o in range(3) for i in range(6)]
-        kps = [ctx.fetch_keypoints(img) for img in range(2 * B)]
-        pairs = [ctx.fetch_stereo_pairs(f) for f in range(B)]
-        outs.append((planes, kps, pairs))
-        ctx.close()
+    for lib in (None, exp):
+        if lib is not None:
+            lib.vo_exp_set(1, 0)
+        try:
+            ctx = vo.Context(rows, cols, B, lib=lib)
+            ctx.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), B)
+            planes = [ctx.fetch_gaussian(img, o, i) for img in (0, 3) for o in range(3) for i in range(6)]
+            kps = [ctx.fetch_keypoints(img) for img in range(2 * B)]
+            pairs = [ctx.fetch_stereo_pairs(f) for f in range(B)]
+            outs.append((planes, kps, pairs))
+            ctx.close()
+        finally:
+            if lib is not None:
+                lib.vo_exp_set(0, 0)
     (p0, k0, s0), (p1, k1, s1) = outs
     for a, b in zip(p0, p1):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))

@@ -40,7 +40,7 @@ def test_roofline_model_matches_survey():
     assert kb["k_blur_fused"][0] == 2 * sum(8 * 5 * r * c + (4 * dims[o + 1][0] * dims[o + 1][1] if o < 3 else 0)
                                             for o, (r, c) in enumerate(dims[:4]))
     assert kb["k_ext_stream<3>"][0] == 2 * sum(4 * 6 * r * c for r, c in dims)
-    # experimental k_octave path (VO_FUSED_OCTAVE=1): octaves 0..3 (>= 256 columns, >= 64 rows)
+    # experimental k_octave path (test build libvo_exp.so, vo_exp_set): octaves 0..3 (>= 256 columns, >= 64 rows)
     # are one launch each (levels, extremum test, next base)
     kf = roofline.kernel_bytes(375, 1242, 2, fused=True)
     assert roofline.fused_octaves(375, 1242, enabled=True) == 4

@@ -20,6 +20,32 @@ def test_expf_nonpos_equals_expf_exhaustively(oracle):
     assert oracle.spec_check_expf_nonpos() == 0
 
 
+def test_rcp_nr_accuracy(oracle):
+    """vo_rcp_nr (integer seed + 3 Newton steps, the reciprocal inside vo_atan2_deg) is within
+    2 ulp of 1/d over the range atan2 feeds it (denominators of gradient components, clamped to
+    >= 1e-30) and well beyond."""
+    rng = np.random.default_rng(3)
+    d = np.concatenate([np.exp2(rng.uniform(-100, 100, 200000)), [1e-30, 1.0, 2.0, 0.75, 510.0, 1024.0]])
+    d = d.astype(np.float32)
+    got = oracle.spec_eval("rcp_nr", d.astype(np.float64)).astype(np.float32)
+    ref = (1.0 / d.astype(np.float64)).astype(np.float32)
+    ulp = np.abs(got.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
+    assert ulp.max() <= 2, ulp.max()
+    assert (ulp == 0).mean() > 0.5
+
+
+def test_sift_wt_is_the_separable_window_weight(oracle):
+    """vo_sift_wt(s, |i|) * vo_sift_wt(s, |j|) (the k_orient / k_desc window weight) agrees with
+    OpenCV's exp((i^2 + j^2) s) to float rounding over the windows' argument range."""
+    s = np.float32(-1.0 / (2.0 * (1.5 * 3.2) ** 2))
+    k = np.arange(0, 15)
+    wk = oracle.spec_eval("sift_wt", np.stack([np.full(len(k), s, np.float64), k], 1).reshape(-1))
+    i, j = np.meshgrid(k, k)
+    w = (wk[i].astype(np.float32) * wk[j].astype(np.float32)).astype(np.float64)
+    ref = np.exp((i * i + j * j) * np.float64(s))
+    assert np.max(np.abs(w - ref) / ref) < 4e-7
+
+
 def test_atan2_deg_accuracy(oracle):
     rng = np.random.default_rng(0)
     y = rng.uniform(-300, 300, 20000)

@@ -1,0 +1,40 @@
+#!/bin/bash
+# One evidence pass on a GPU box (run through gpurun from the repo root):
+#   bash tools/gpu_run.sh <outdir> [steps...]
+# steps (default: tests smoke bench): tests | smoke | bench | distbench | kprof | seqprof | gpuonly:<pytest -k expr>
+# Every GPU step has its own time limit and the chain stops at the first failure.
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${1:?outdir}; shift; mkdir -p $O
+STEPS=${@:-tests smoke bench}
+for st in $STEPS; do
+  case $st in
+  tests)
+    timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/gpu_tests.log 2>&1 \
+      || { tail -40 $O/gpu_tests.log; exit 1; }
+    tail -1 $O/gpu_tests.log ;;
+  gpuonly:*)
+    timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -k "${st#gpuonly:}" > $O/gpu_sel.log 2>&1 \
+      || { tail -40 $O/gpu_sel.log; exit 1; }
+    tail -1 $O/gpu_sel.log ;;
+  smoke)
+    timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+    tail -1 $O/smoke.log ;;
+  bench)
+    timeout -k 10 600 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+    python3 -c "import json;d=json.load(open('$O/bench.json'));r=d['roofline'];t=d['timed_runs'];print('bench',round(d['value']),round(d['ms_per_step'],3),t['ms_per_step'],r['kernel'],round(r['frac'],3),'h2d',round(d['h2d']['ms_per_step'],3));print('full',round(d['full_path']['value']),'large',round(d['large']['value']),'cpu',d['cpu_baseline']['value'])" ;;
+  distbench)
+    VO_BENCH_FORCE_DIST=1 timeout -k 10 600 python3 bench.py --no-cpu --large-batch 0 > $O/distbench.json 2> $O/distbench.err \
+      || { tail -20 $O/distbench.err; exit 1; }
+    python3 -c "import json;d=json.load(open('$O/distbench.json'));f=d['full_path'];print('distbench',d['config']['process_group'],round(d['value']),'full',round(f['value']),f['landmark_rows'],f['accuracy']['ate_rmse_m'])" ;;
+  kprof)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kprof -o k -- python3 bench.py --steps 10 --runs 1 --warmup 2 --no-cpu --seq-frames 0 --large-batch 0 > $O/kprof_bench.json 2> $O/kprof.err
+    find $O/kprof -name "*kernel_trace.csv" -delete
+    echo kprof-done ;;
+  seqprof)
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/seqprof -o k -- python3 bench.py --steps 2 --runs 1 --warmup 1 --no-cpu --large-batch 0 > $O/seqprof_bench.json 2> $O/seqprof.err
+    find $O/seqprof -name "*kernel_trace.csv" -delete
+    echo seqprof-done ;;
+  *) echo "unknown step $st"; exit 2 ;;
+  esac
+done
