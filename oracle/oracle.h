@@ -46,6 +46,9 @@ long oracle_pyramid(const uint8_t* img, int rows, int cols, int ld, const vo_sif
 /* matchFeatures (VO.m:87 ...). pairs 1-based. returns n_pairs (may exceed cap). */
 int oracle_match(const uint8_t* F1, int n1, const uint8_t* F2, int n2, const vo_match_params* p,
                  uint32_t* pairs, int capacity);
+/* matchFeatures on general single features (libvo vo_match_f32 for non-u8-valued rows) */
+int oracle_match_f32(const float* F1, int n1, int ld1, const float* F2, int n2, int ld2, int col_major,
+                     const vo_match_params* p, uint32_t* pairs, int capacity);
 
 /* find_remaining_points (VO.m:280-334). idx_out[K][3] 1-based. returns K. */
 int oracle_track(const uint8_t* old_l, const uint8_t* old_r, int n_old,

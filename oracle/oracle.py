@@ -104,6 +104,8 @@ def lib(cv: bool = False):
         L.oracle_pyramid.argtypes = [P(C.c_uint8), C.c_int, C.c_int, C.c_int, P(SiftParams), P(C.c_float)]
         L.oracle_pyramid.restype = C.c_long
         L.oracle_match.argtypes = [P(C.c_uint8), C.c_int, P(C.c_uint8), C.c_int, P(MatchParams), P(C.c_uint32), C.c_int]
+        L.oracle_match_f32.argtypes = [P(C.c_float), C.c_int, C.c_int, P(C.c_float), C.c_int, C.c_int, C.c_int,
+                                       P(MatchParams), P(C.c_uint32), C.c_int]
         L.oracle_track.argtypes = [P(C.c_uint8), P(C.c_uint8), C.c_int, P(C.c_uint8), C.c_int, P(C.c_uint8), C.c_int,
                                    P(MatchParams), P(C.c_uint32), C.c_int]
         L.oracle_triangulate.argtypes = [P(C.c_float), P(C.c_float), C.c_int, P(C.c_double), P(C.c_double), P(C.c_double)]
@@ -186,6 +188,18 @@ def match(F1: np.ndarray, F2: np.ndarray, params: MatchParams | None = None, cv:
     pairs = np.zeros((cap, 2), np.uint32)
     n = lib(cv).oracle_match(_p(F1, C.c_uint8), F1.shape[0], _p(F2, C.c_uint8), F2.shape[0],
                            C.byref(params or match_params()), _p(pairs, C.c_uint32), cap)
+    return pairs[:n].copy()
+
+
+def match_f32(F1: np.ndarray, F2: np.ndarray, params: MatchParams | None = None) -> np.ndarray:
+    """matchFeatures on general single features (the float spec of libvo vo_match_f32):
+    1-based uint32 (P, 2).  Rows are passed row-major (ld = 128)."""
+    F1 = np.ascontiguousarray(F1, np.float32).reshape(-1, 128)
+    F2 = np.ascontiguousarray(F2, np.float32).reshape(-1, 128)
+    cap = max(F1.shape[0], 1)
+    pairs = np.zeros((cap, 2), np.uint32)
+    n = lib().oracle_match_f32(_p(F1, C.c_float), F1.shape[0], 128, _p(F2, C.c_float), F2.shape[0], 128, 0,
+                               C.byref(params or match_params()), _p(pairs, C.c_uint32), cap)
     return pairs[:n].copy()
 
 

@@ -123,6 +123,56 @@ int oracle_match(const uint8_t* F1, int n1, const uint8_t* F2, int n2, const vo_
     return P;
 }
 
+/* matchFeatures on general single-precision features (libvo vo_match_f32 when the rows are not
+ * u8-valued): rows normalised to unit L2 (a_k = f_k / sqrtf(fmaf chain of f_k^2), zero rows stay
+ * zero), SSD as the fmaf chain of (a_k - b_k)^2 over k = 0..127, then the u8 path's selection
+ * (smallest / second smallest, ties to the lowest F2 row; SSD <= 0.04 * MatchThreshold; ratio
+ * <= MaxRatio).  Element k of row i: F[col_major ? k * ld + i : i * ld + k]. */
+static void norm_rows_f32(const float* F, int n, int ld, int col_major, float* out)
+{
+    for (int i = 0; i < n; ++i) {
+        float n2 = 0.0f;
+        for (int k = 0; k < VO_DESC_LEN; ++k) {
+            const float v = col_major ? F[(size_t)k * ld + i] : F[(size_t)i * ld + k];
+            n2 = fmaf(v, v, n2);
+        }
+        const float nrm = sqrtf(n2);
+        for (int k = 0; k < VO_DESC_LEN; ++k) {
+            const float v = col_major ? F[(size_t)k * ld + i] : F[(size_t)i * ld + k];
+            out[(size_t)i * VO_DESC_LEN + k] = nrm > 0.0f ? v / nrm : 0.0f;
+        }
+    }
+}
+
+int oracle_match_f32(const float* F1, int n1, int ld1, const float* F2, int n2, int ld2, int col_major,
+                     const vo_match_params* p, uint32_t* pairs, int capacity)
+{
+    float* a = (float*)malloc(sizeof(float) * VO_DESC_LEN * (size_t)(n1 > 0 ? n1 : 1));
+    float* b = (float*)malloc(sizeof(float) * VO_DESC_LEN * (size_t)(n2 > 0 ? n2 : 1));
+    norm_rows_f32(F1, n1, ld1, col_major, a);
+    norm_rows_f32(F2, n2, ld2, col_major, b);
+    const float T = p->match_threshold * 0.04f;
+    int P = 0;
+    for (int i = 0; i < n1; ++i) {
+        float best = INFINITY, second = INFINITY;
+        int bidx = -1;
+        for (int j = 0; j < n2; ++j) {
+            float s = 0.0f;
+            for (int k = 0; k < VO_DESC_LEN; ++k) {
+                const float d = a[(size_t)i * VO_DESC_LEN + k] - b[(size_t)j * VO_DESC_LEN + k];
+                s = fmaf(d, d, s);
+            }
+            if (s < best) { second = best; best = s; bidx = j; }
+            else if (s < second) second = s;
+        }
+        if (bidx < 0 || !(best <= T) || !(best / second <= p->max_ratio)) continue;
+        if (P < capacity) { pairs[2 * P] = (uint32_t)i + 1; pairs[2 * P + 1] = (uint32_t)bidx + 1; }
+        P++;
+    }
+    free(a); free(b);
+    return P;
+}
+
 /* ======================================================================= */
 /* find_remaining_points (VO.m:280-334) as index composition                 */
 /* ======================================================================= */

@@ -427,6 +427,77 @@ void pack_f32_desc_launch(const float* F, int n, int ld, int col_major, uint8_t*
     VO_LAUNCH(k_pack_f32_desc, dim3(blocks), dim3(256), 0, s, F, n, ld, col_major, out, bad);
 }
 
+// ---------------------------------------------------------------------------
+// matchFeatures on general single-precision features (vo_match_f32 when the rows are not
+// u8-valued SIFT descriptors).  Spec, restated by the oracle's oracle_match_f32 (vo_ref.c):
+//   a_k = f_k / nrm (0 if nrm == 0), nrm = sqrtf(fmaf chain of f_k^2 over k = 0..127);
+//   ssd(i, j) = fmaf chain of (a_k - b_k)^2 over k = 0..127;
+//   best / second = smallest / second smallest ssd of row i (multiset; ties -> lowest j);
+//   accept best <= 0.04 * MatchThreshold and best / second <= MaxRatio (the u8 path's rule).
+// k_f32_norm: one thread per row; F2 rows are written transposed ([128][n2]) so k_match_f32's
+// lanes (one F2 column each) read them coalesced.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_f32_norm(const float* __restrict__ F, int n, int ld, int col_major, int transpose,
+                                                  float* __restrict__ out)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    auto at = [&](int k) { return col_major ? F[(size_t)k * ld + i] : F[(size_t)i * ld + k]; };
+    float n2 = 0.0f;
+    for (int k = 0; k < VO_DESC_LEN; ++k) { const float v = at(k); n2 = fmaf(v, v, n2); }
+    const float nrm = sqrtf(n2);
+    for (int k = 0; k < VO_DESC_LEN; ++k) {
+        const float v = nrm > 0.0f ? at(k) / nrm : 0.0f;
+        out[transpose ? (size_t)k * n + i : (size_t)i * VO_DESC_LEN + k] = v;
+    }
+}
+
+// one wave per F1 row (grid-stride): the row in LDS (broadcast reads), lane l scores columns
+// l, l + 64, ... with the sequential fmaf chain, keeps its own top-2, and the wave merges the
+// 64 top-2s with the order-free (value, index) rule; res[i] = accepted column or -1
+__global__ __launch_bounds__(64) void k_match_f32(const float* __restrict__ A, int n1, const float* __restrict__ BT, int n2,
+                                                  float T, float max_ratio, int* __restrict__ res)
+{
+    __shared__ float a[VO_DESC_LEN];
+    const int lane = threadIdx.x;
+    for (int i = blockIdx.x; i < n1; i += gridDim.x) {
+        a[lane] = A[(size_t)i * VO_DESC_LEN + lane];
+        a[lane + 64] = A[(size_t)i * VO_DESC_LEN + lane + 64];
+        __syncthreads();
+        float best = INFINITY, second = INFINITY;
+        int bidx = -1;
+        for (int j = lane; j < n2; j += 64) {
+            float ssd = 0.0f;
+            for (int k = 0; k < VO_DESC_LEN; ++k) {
+                const float d = a[k] - BT[(size_t)k * n2 + j];
+                ssd = fmaf(d, d, ssd);
+            }
+            if (ssd < best) { second = best; best = ssd; bidx = j; }
+            else if (ssd < second) second = ssd;
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const float b2 = __shfl_xor(best, off), s2 = __shfl_xor(second, off);
+            const int i2 = __shfl_xor(bidx, off);
+            const float ns = fminf(fminf(second, s2), fmaxf(best, b2));
+            if (i2 >= 0 && (bidx < 0 || b2 < best || (b2 == best && i2 < bidx))) { best = b2; bidx = i2; }
+            second = ns;
+        }
+        if (lane == 0) res[i] = (bidx >= 0 && best <= T && best / second <= max_ratio) ? bidx : -1;
+        __syncthreads();
+    }
+}
+
+void match_f32_launch(const float* F1, int n1, int ld1, const float* F2, int n2, int ld2, int col_major, float* A, float* BT,
+                      int* res, const vo_match_params& p, hipStream_t s)
+{
+    if (n1 <= 0) return;
+    VO_LAUNCH(k_f32_norm, dim3((n1 + 255) / 256), dim3(256), 0, s, F1, n1, ld1, col_major, 0, A);
+    if (n2 > 0) VO_LAUNCH(k_f32_norm, dim3((n2 + 255) / 256), dim3(256), 0, s, F2, n2, ld2, col_major, 1, BT);
+    VO_LAUNCH(k_match_f32, dim3(std::min(n1, 8192)), dim3(64), 0, s, A, n1, BT, n2, p.match_threshold * 0.04f, p.max_ratio,
+              res);
+}
+
 void desc_meta_launch(const uint8_t* desc, DescMeta* meta, int n, hipStream_t s)
 {
     if (n <= 0) return;

@@ -102,6 +102,11 @@ struct vo_ctx {
     DescMeta* d_fm[2] = {nullptr, nullptr};
     int* d_fn = nullptr;             // [2]
     float* d_ff[2] = {nullptr, nullptr};   // vo_match_f32 staging (single descriptors as MATLAB holds them)
+    // vo_match_f32 on general (non-u8-valued) features: normalised F1, transposed F2, per-row result
+    // (allocated on first use)
+    float* d_fa = nullptr;
+    float* d_fbt = nullptr;
+    int* d_fres = nullptr;
     int* d_bad = nullptr;
     int* d_mi = nullptr; int* d_mj = nullptr; int* d_mn = nullptr;
     GeomBuffers gb;
@@ -209,6 +214,7 @@ static void destroy_buffers(vo_ctx* c)
     hipFree(c->d_py); hipFree(c->d_jobs); hipFree(c->d_pair_i); hipFree(c->d_pair_j); hipFree(c->d_pair_n);
     hipFree(c->d_img); hipFree(c->d_cm); hipFree(c->d_fd[0]); hipFree(c->d_fd[1]); hipFree(c->d_fm[0]); hipFree(c->d_fm[1]);
     hipFree(c->d_ff[0]); hipFree(c->d_ff[1]); hipFree(c->d_bad);
+    hipFree(c->d_fa); hipFree(c->d_fbt); hipFree(c->d_fres);
     hipFree(c->d_fn); hipFree(c->d_mi); hipFree(c->d_mj); hipFree(c->d_mn);
 }
 
@@ -561,12 +567,34 @@ int vo_match_f32(vo_ctx* c, const float* F1, int n1, int ld1, const float* F2, i
         HIPC(c, hipMemcpyAsync(c->d_ff[s], src[s], sizeof(float) * elems, hipMemcpyHostToDevice, c->stream));
         pack_f32_desc_launch(c->d_ff[s], n[s], ld[s], col_major, c->d_fd[s], c->d_bad, c->stream);
     }
-    int rc = match_staged(c, n1, n2, pairs, capacity, n_pairs, "vo_match_f32");
-    if (rc && rc != VO_ERR_CAPACITY) return rc;
     int bad = 0;
-    HIPC(c, hipMemcpy(&bad, c->d_bad, sizeof(int), hipMemcpyDeviceToHost));
-    if (bad) return fail(c, VO_ERR_ARG, "vo_match_f32: descriptor values must be integers in [0, 255] (SIFT)");
-    return rc;
+    HIPC(c, hipMemcpyAsync(&bad, c->d_bad, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    int rc = finish(c);
+    if (rc) return rc;
+    // u8-valued rows (libvo / SIFT descriptors, what VO.m passes): the exact-integer spec of the
+    // hot path; any other single features: the float SSD spec (match_f32_launch)
+    if (!bad) return match_staged(c, n1, n2, pairs, capacity, n_pairs, "vo_match_f32");
+    if (!c->d_fa) {
+        const size_t fb = sizeof(float) * (size_t)c->sb.kp_cap * VO_DESC_LEN;
+        hipError_t e;
+        if ((e = hipMalloc((void**)&c->d_fa, fb)) != hipSuccess || (e = hipMalloc((void**)&c->d_fbt, fb)) != hipSuccess ||
+            (e = hipMalloc((void**)&c->d_fres, sizeof(int) * c->sb.kp_cap)) != hipSuccess)
+            return fail(c, VO_ERR_HIP, "vo_match_f32: %s", hipGetErrorString(e));
+    }
+    match_f32_launch(c->d_ff[0], n1, ld1, c->d_ff[1], n2, ld2, col_major, c->d_fa, c->d_fbt, c->d_fres, c->mp, c->stream);
+    std::vector<int> res((size_t)n1 + 1);
+    if (n1) HIPC(c, hipMemcpyAsync(res.data(), c->d_fres, sizeof(int) * n1, hipMemcpyDeviceToHost, c->stream));
+    rc = finish(c);
+    if (rc) return rc;
+    int P = 0;
+    for (int i = 0; i < n1; ++i) {
+        if (res[i] < 0) continue;
+        if (pairs && P < capacity) { pairs[2 * P] = (uint32_t)i + 1; pairs[2 * P + 1] = (uint32_t)res[i] + 1; }
+        ++P;
+    }
+    if (n_pairs) *n_pairs = P;
+    if (P > capacity) return fail(c, VO_ERR_CAPACITY, "vo_match_f32: %d pairs exceed capacity %d", P, capacity);
+    return VO_OK;
 }
 
 // SIFT + stereo match on B frames already in device memory.
@@ -1186,7 +1214,9 @@ int vo_estworldpose(vo_ctx* c, const double* img, const double* world, int n, co
     if (!c || n < 0 || (n && (!img || !world)) || !K9 || !T) return fail(c, VO_ERR_ARG, "vo_estworldpose: bad arguments");
     if (n > c->sb.kp_cap) return fail(c, VO_ERR_CAPACITY, "vo_estworldpose: %d points exceed max_keypoints", n);
     const vo_ransac_params rp = params ? *params : c->rp;
-    if (rp.max_num_trials > c->gb.n_hyp) return fail(c, VO_ERR_ARG, "vo_estworldpose: max_num_trials > context's");
+    if (rp.max_num_trials > c->gb.n_hyp)
+        return fail(c, VO_ERR_ARG, "vo_estworldpose: MaxNumTrials %d exceeds the context's %d hypothesis slots (vo_create ransac.max_num_trials)",
+                    rp.max_num_trials, c->gb.n_hyp);
     if (n_inliers) *n_inliers = 0;
     if (n < 4) return fail(c, VO_ERR_TOO_FEW_POINTS, "estworldpose: need at least 4 points, got %d", n);
     BEGIN_CALL(c);

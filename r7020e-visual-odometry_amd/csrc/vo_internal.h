@@ -230,5 +230,9 @@ void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, con
                   hipStream_t s);
 void desc_meta_launch(const uint8_t* desc, DescMeta* meta, int n, hipStream_t s);
 void pack_f32_desc_launch(const float* F, int n, int ld, int col_major, uint8_t* out, int* bad, hipStream_t s);
+// matchFeatures on general single features (not u8-valued): normalised rows A [n1][128], F2
+// normalised and transposed into BT [128][n2], res[i] = accepted F2 column of row i or -1
+void match_f32_launch(const float* F1, int n1, int ld1, const float* F2, int n2, int ld2, int col_major, float* A, float* BT,
+                      int* res, const vo_match_params& p, hipStream_t s);
 
 }  // namespace vo

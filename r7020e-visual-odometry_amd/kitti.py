@@ -265,8 +265,11 @@ def _pipelined(ctx, batches, dev, on_collect=None) -> list:
         if isinstance(L, torch.Tensor):                       # device-resident frames
             dl, dr = L.contiguous(), R.contiguous()
             # the frames' producer (and any .contiguous() copy) ran on torch's current stream,
-            # which libvo's non-blocking streams do not wait for
-            torch.cuda.current_stream(dl.device).synchronize()
+            # which libvo's non-blocking streams do not wait for: wait for it only when it still
+            # has work queued (a resident, already-synchronised sequence costs a query per batch)
+            ts = torch.cuda.current_stream(dl.device)
+            if not ts.query():
+                ts.synchronize()
             L = L.cpu().numpy() if on_collect is not None else None
         else:
             dl = torch.from_numpy(L).pin_memory().to(dev, non_blocking=True)

@@ -107,10 +107,37 @@ def test_match_f32_storage_orders_equal_u8_match(vo, oracle, syn):
     pad[:, :128] = fl
     assert np.array_equal(ctx.match_f32(pad[:, :128], fr), ref)                               # row stride 160
     assert len(ctx.match_f32(np.zeros((0, 128), np.float32), fr)) == 0
-    bad = fl.copy()
-    bad[3, 7] = 0.5
-    with pytest.raises(vo.VOError):
-        ctx.match_f32(bad, fr)
+    # one non-integer value: the whole call takes the float SSD spec (oracle_match_f32)
+    gen = fl.copy()
+    gen[3, 7] = 0.5
+    assert np.array_equal(ctx.match_f32(gen, fr), oracle.match_f32(gen, fr))
+    ctx.close()
+
+
+@pytest.mark.parametrize("n1,n2", [(300, 500), (1, 1), (7, 1), (0, 5), (5, 0), (2100, 2300)])
+def test_match_f32_general_features_equal_oracle(vo, oracle, n1, n2):
+    """vo_match_f32 on general single features (not u8-valued: matchFeatures for any other MATLAB
+    caller of the path-shadowed function) == the oracle's float SSD restatement bit for bit, in
+    both storage orders: near-duplicate rows (matches), exact duplicates (0/0 ratio: rejected),
+    a single candidate (ratio 0: accepted), zero rows, and F2 beyond one 64-column lane sweep."""
+    rng = np.random.default_rng(n1 * 7 + n2)
+    F2 = rng.standard_normal((n2, 128)).astype(np.float32)
+    F1 = rng.standard_normal((n1, 128)).astype(np.float32)
+    if n1 and n2:
+        k = min(n1, n2) // 2
+        pick = rng.integers(0, n2, k)
+        F1[:k] = F2[pick] + 0.02 * rng.standard_normal((k, 128)).astype(np.float32)   # near duplicates
+        if n2 > 3 and n1 > k + 1:
+            F2[1] = F2[0]
+            F1[k] = F2[0]                                                             # exact duplicate pair in F2
+            F1[k + 1] = 0.0                                                           # zero row
+    ref = oracle.match_f32(F1, F2)
+    ctx = vo.Context(375, 1242, 1)
+    got = ctx.match_f32(F1, F2)
+    assert np.array_equal(got, ref), (len(got), len(ref))
+    assert np.array_equal(ctx.match_f32(np.asfortranarray(F1), np.asfortranarray(F2)), ref)
+    if n1 > 10 and n2 > 10:
+        assert len(ref) >= min(n1, n2) // 2 - 2
     ctx.close()
 
 

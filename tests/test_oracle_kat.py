@@ -277,3 +277,26 @@ def test_sequence_tracks_ground_truth(oracle, syn):
     err = np.linalg.norm(outs["pose"][:, :3, 3] - gt[:, :3, 3], axis=1)
     assert err.max() < 0.5
     assert lm.shape[0] == outs["n_landmarks"].sum()
+
+
+def test_match_f32_known_answers(oracle):
+    """The float SSD restatement of matchFeatures (oracle_match_f32, libvo's spec for non-u8
+    features): hand-built rows with known nearest / second-nearest neighbours.  Scale invariance
+    (rows are normalised), the 0.04 SSD threshold, the 0.6 ratio, a single candidate, duplicate
+    F2 rows (0/0 ratio: rejected) and a zero row."""
+    e = np.eye(128, dtype=np.float32)
+    F2 = np.stack([e[0], e[1], e[2], e[2]])                        # rows 2 and 3 duplicates
+    q = lambda v: (v / np.linalg.norm(v)).astype(np.float32)
+    F1 = np.stack([
+        5.0 * q(e[0] + 0.05 * e[5]),        # near e0 (ssd ~ 0.0025), far from e1: accepted -> 1
+        q(e[1] + 0.3 * e[0]),               # ssd to e1 ~ 0.087 > 0.04: rejected by threshold
+        q(e[2] + 0.01 * e[7]),              # nearest rows 2 and 3 tie: best/second = 1: rejected
+        np.zeros(128, np.float32),          # zero row: ssd 1 to everything: rejected
+        q(e[1] + 0.1 * e[9]),               # ssd ~ 0.0099 to e1, ~ 2 to the rest: accepted -> 2
+    ])
+    got = oracle.match_f32(F1, F2)
+    assert got.tolist() == [[1, 1], [5, 2]]
+    # one candidate: the ratio is 0, only the threshold decides
+    assert oracle.match_f32(F1[:1], e[:1]).tolist() == [[1, 1]]
+    assert oracle.match_f32(F1[1:2], e[1:2]).tolist() == []
+    assert oracle.match_f32(F1[:0], F2).shape == (0, 2) and oracle.match_f32(F1, F2[:0]).shape == (0, 2)
