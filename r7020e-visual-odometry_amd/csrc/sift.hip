@@ -805,12 +805,17 @@ __global__ __launch_bounds__(64, (RAD <= 6 || CPL == 2) ? 3 : 2) void k_blur_str
     const int THb = min(TH, (R - y0 + BS_P - 1) / BS_P * BS_P);
     const size_t os = img * splane, od = img * dplane;
     U8Src u8{nullptr, 0, in_rows, in_cols};
+    int margin = 0;
     if (TAG & 4) {
         u8.p = ((img & 1) ? isrc.right : isrc.left) + (size_t)(img >> 1) * isrc.frame_stride;
         u8.ld = isrc.ld;
+        // the interior form reads source bytes g2-1 .. g2+2 for outputs 2 g2 .. 2 g2 + 3 with no
+        // clamp: the span must end >= 2 columns before the plane's edge (16: the strips of the
+        // validated pre-staging layout)
+        margin = 16;
     }
     float* const nbo = K.nb ? K.nb + od : nullptr;
-    if (x0 - RH < 0 || (XCH ? x0 - RH + 64 * CPL : x0 + SW + RH) > C)
+    if (x0 - RH < 0 || (XCH ? x0 - RH + 64 * CPL : x0 + SW + RH) + margin > C)
         blur_stream_body<RAD, true, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, THb, rb, u8, nbo, stg);
     else
         blur_stream_body<RAD, false, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, THb, rb, u8, nbo, stg);

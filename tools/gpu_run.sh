@@ -1,7 +1,8 @@
 #!/bin/bash
 # One evidence pass on a GPU box (run through gpurun from the repo root):
 #   bash tools/gpu_run.sh <outdir> [steps...]
-# steps (default: tests smoke bench): tests | smoke | bench | distbench | kprof | seqprof | gpuonly:<pytest -k expr>
+# steps (default: tests smoke bench): tests | smoke | bench | distbench | kprof | seqprof | attr | probe:<tools binary>
+#   | gpuonly:<pytest -k expr>
 # Every GPU step has its own time limit and the chain stops at the first failure.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -35,6 +36,12 @@ for st in $STEPS; do
     timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/seqprof -o k -- python3 bench.py --steps 2 --runs 1 --warmup 1 --no-cpu --large-batch 0 > $O/seqprof_bench.json 2> $O/seqprof.err
     find $O/seqprof -name "*kernel_trace.csv" -delete
     echo seqprof-done ;;
+  probe:*)
+    b=${st#probe:}; timeout -k 10 120 ./tools/$b > $O/$b.txt 2>&1 || { cat $O/$b.txt; exit 1; }
+    cat $O/$b.txt ;;
+  attr)
+    timeout -k 10 400 python3 tools/fullpath_attr.py 1024 64 > $O/fullpath_attr.json 2> $O/fullpath_attr.err || { tail -20 $O/fullpath_attr.err; exit 1; }
+    python3 -c "import json;d=json.load(open('$O/fullpath_attr.json'));print('attr',d['ms_per_batch'])" ;;
   *) echo "unknown step $st"; exit 2 ;;
   esac
 done
