@@ -845,6 +845,50 @@ __global__ __launch_bounds__(256) void k_down(const float* __restrict__ src, siz
 #define VO_SMALL_PX 9216          // 3 planes + the next base fit in 160 KB of LDS
 #define VO_SMALL_T 1024
 
+// Register-blocked passes of k_small_pyr: one thread computes SMV consecutive outputs along the
+// filter direction from the SMV + 2r inputs it reads once (reflect-101 through the tables only
+// near the plane's edges), so a tap costs no LDS reads: the per-tap form read two table entries
+// and two values per tap and output (~52 LDS reads per output at r = 13) and was LDS-bound.
+// Per output: acc = k0 s0; acc = fmaf(kj, s[-j] + s[+j], acc), j = 1..r (the spec's order).
+constexpr int SMV = 8;
+template <int RAD>
+__device__ __forceinline__ void small_pass(const float* __restrict__ src, float* __restrict__ dst, float* __restrict__ gdst,
+                                           int gpitch, int R, int C, bool rows, const float* __restrict__ kk,
+                                           const int* __restrict__ tab, int tid)
+{
+    // rows: items (y, x0 = 8q) along rows; else items (x, y0 = 8q) down columns.  Consecutive
+    // threads take consecutive lines (row pass: rows C floats apart, C odd or not a multiple of
+    // 64 at these octaves; column pass: adjacent columns), not consecutive runs of one line (8
+    // floats apart: an 8-way LDS bank conflict)
+    const int len = rows ? C : R, other = rows ? R : C, runs = (len + SMV - 1) / SMV;
+    float k[RAD + 1];
+#pragma unroll
+    for (int j = 0; j <= RAD; ++j) k[j] = kk[j];
+    for (int it = tid; it < other * runs; it += VO_SMALL_T) {
+        const int q = it / other, line = it - q * other, p0 = q * SMV;
+        const int stride = rows ? 1 : C;
+        const float* s0 = rows ? src + line * C : src + line;
+        float w[SMV + 2 * RAD];
+        if (p0 - RAD >= 0 && p0 + SMV - 1 + RAD < len) {
+#pragma unroll
+            for (int j = 0; j < SMV + 2 * RAD; ++j) w[j] = s0[(p0 - RAD + j) * stride];
+        } else {
+#pragma unroll
+            for (int j = 0; j < SMV + 2 * RAD; ++j) w[j] = s0[tab[min(p0 + j, len - 1 + 2 * RAD)] * stride];
+        }
+#pragma unroll
+        for (int v = 0; v < SMV; ++v) {
+            if (p0 + v >= len) break;
+            float acc = k[0] * w[RAD + v];
+#pragma unroll
+            for (int j = 1; j <= RAD; ++j) acc = fmaf(k[j], w[RAD + v - j] + w[RAD + v + j], acc);
+            const int y = rows ? line : p0 + v, x = rows ? p0 + v : line;
+            dst[y * C + x] = acc;
+            if (gdst) gdst[(size_t)y * gpitch + x] = acc;
+        }
+    }
+}
+
 __global__ __launch_bounds__(VO_SMALL_T) void k_small_pyr(const Pyramid* __restrict__ py, float* __restrict__ arena,
                                                           int o_first, int rtab)
 {
@@ -884,20 +928,32 @@ __global__ __launch_bounds__(VO_SMALL_T) void k_small_pyr(const Pyramid* __restr
             for (int t = tid; t < R + 2 * r; t += VO_SMALL_T) ridx[t] = vo_reflect101(t - r, R);
             for (int t = tid; t < C + 2 * r; t += VO_SMALL_T) cidx[t] = vo_reflect101(t - r, C);
             __syncthreads();
-            for (int e = tid; e < RC; e += VO_SMALL_T) {                 // row pass
-                const int y = e / C, x = e - y * C;
-                const float* row = cur + y * C;
-                float acc = kk[0] * row[x];
-                for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], row[cidx[x + r - j]] + row[cidx[x + r + j]], acc);
-                tmp[e] = acc;
-            }
-            __syncthreads();
-            for (int e = tid; e < RC; e += VO_SMALL_T) {                 // column pass
-                const int y = e / C, x = e - y * C;
-                float acc = kk[0] * tmp[e];
-                for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], tmp[ridx[y + r - j] * C + x] + tmp[ridx[y + r + j] * C + x], acc);
-                nxt[e] = acc;
-                gplane[g.g_off[i] + (size_t)y * g.pitch + x] = acc;
+            float* const gl = gplane + g.g_off[i];
+            switch (r) {                                                  // the default sigmas' radii
+#define VO_SMALL_R(RR)                                                                        \
+    case RR:                                                                                  \
+        small_pass<RR>(cur, tmp, nullptr, 0, R, C, true, kk, cidx, tid);                      \
+        __syncthreads();                                                                      \
+        small_pass<RR>(tmp, nxt, gl, g.pitch, R, C, false, kk, ridx, tid);                    \
+        break;
+            VO_SMALL_R(5) VO_SMALL_R(6) VO_SMALL_R(8) VO_SMALL_R(10) VO_SMALL_R(13)
+#undef VO_SMALL_R
+            default:
+                for (int e = tid; e < RC; e += VO_SMALL_T) {                 // row pass
+                    const int y = e / C, x = e - y * C;
+                    const float* row = cur + y * C;
+                    float acc = kk[0] * row[x];
+                    for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], row[cidx[x + r - j]] + row[cidx[x + r + j]], acc);
+                    tmp[e] = acc;
+                }
+                __syncthreads();
+                for (int e = tid; e < RC; e += VO_SMALL_T) {                 // column pass
+                    const int y = e / C, x = e - y * C;
+                    float acc = kk[0] * tmp[e];
+                    for (int j = 1; j <= r; ++j) acc = fmaf(kk[j], tmp[ridx[y + r - j] * C + x] + tmp[ridx[y + r + j] * C + x], acc);
+                    nxt[e] = acc;
+                    gl[(size_t)y * g.pitch + x] = acc;
+                }
             }
             __syncthreads();
             if (i == L && o + 1 < py->n_oct) {                           // next octave's base: decimated G_L
