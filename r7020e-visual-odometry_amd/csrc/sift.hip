@@ -519,8 +519,12 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
         const int sr1 = min(u8.rows - 1, (ymax >> 1) + 1);
         const int total = (sr1 - sr0 + 1) * SWD;           // <= bs_u8_rows(RAD) * SWD (kBaseMaxTH)
         delta = (uint32_t)(reinterpret_cast<uintptr_t>(u8.p) & 3);
-        const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(u8.p - delta), 0, (int)(delta + (uint32_t)(u8.rows - 1) * (uint32_t)u8.ld + (uint32_t)u8.cols), 0x00020000);
+        // range = the image's last byte rounded up to its dword: a buffer load returns 0 for a
+        // whole dword that crosses the range's end, which would drop the last row's final bytes;
+        // the rounded range stays inside that 4-B aligned word, so it never reaches another page
+        const uint32_t span = delta + (uint32_t)(u8.rows - 1) * (uint32_t)u8.ld + (uint32_t)u8.cols;
+        const __amdgpu_buffer_rsrc_t rs_in =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(u8.p - delta), 0, (int)((span + 3u) & ~3u), 0x00020000);
         constexpr int SCH = 16;                            // loads in flight per lane per round
         for (int t0 = 0; t0 < total; t0 += 64 * SCH) {
             uint32_t v[SCH];
@@ -783,8 +787,11 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
 // upsample of the u8 image fused (isrc); instrumentation variants used only by
 // tools/blur_probe.hip: 2 cached stores, 8 no row pass, 16 no column pass,
 // 32 no LDS staging, 64 no halo loads.  CPL: columns per lane (4 or 2).
+#ifndef VO_BLUR_OCC3_MAXR
+#define VO_BLUR_OCC3_MAXR 6       // radii up to this run at 3 waves per SIMD (168 VGPRs), larger at 2
+#endif
 template <int RAD, int TAG, int CPL = 4>
-__global__ __launch_bounds__(64, (RAD <= 6 || CPL == 2) ? 3 : 2) void k_blur_stream(
+__global__ __launch_bounds__(64, (RAD <= VO_BLUR_OCC3_MAXR || CPL == 2) ? 3 : 2) void k_blur_stream(
     const float* __restrict__ src, size_t splane, size_t dplane, int pitch, int R, int C, float* __restrict__ g_out, Kern K,
     int n_strips, int n_bands, int TH, ImageSrc isrc, int in_rows, int in_cols)
 {

@@ -7,7 +7,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [(375, 1242), (376, 1241), (240, 700), (97, 131), (131, 97), (400, 1800)]
+SIZES = [(375, 1242), (376, 1241), (240, 700), (97, 131), (131, 97), (400, 1800), (77, 101)]
 
 
 def _planes(oracle, img, L=3):

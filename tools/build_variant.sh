@@ -10,7 +10,8 @@ OUT=$D/tools/variants/$NAME
 mkdir -p $OUT/obj
 cd ${VO_SRC:-$D/r7020e-visual-odometry_amd/csrc}
 FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I${VO_INC:-$D/include} -I. $*"
-for f in sift octave match geom vo_api; do
+SRCS="sift match geom vo_api"; case "$*" in *VO_EXPERIMENTAL*) SRCS="$SRCS octave";; esac
+for f in $SRCS; do
   X=""; [ $f = match ] && X="-mllvm -amdgpu-mfma-vgpr-form"
   /opt/rocm/bin/hipcc $FL $X -c $f.hip -o $OUT/obj/$f.o &
 done

@@ -105,6 +105,121 @@ __global__ __launch_bounds__(128) void k_decoupled(const float* __restrict__ a, 
     }
 }
 
+// the blur-shaped comparison: W dependent packed FMAs per row vector (about the level blur's
+// per-row VALU), occupancy capped by dynamic LDS at the blur's 2 waves per SIMD.
+//   coupledW: one wave per unit, P = 4 rows ahead, stores in the same vmcnt queue
+//   dec3W:    1 loader wave + 3 compute waves per workgroup (3 bands of one strip), the loader
+//             keeping 2 blocks of 4 rows per band in flight in registers, an LDS ring of 2
+//             blocks per band; compute waves never wait on vmcnt
+template <int W>
+__device__ __forceinline__ f4 work(f4 v)
+{
+    f4 a = v;
+#pragma unroll
+    for (int i = 0; i < W; ++i) a = a * 0.999f + v;
+    return a;
+}
+
+template <int W>
+__global__ __launch_bounds__(64) void k_coupledW(const float* __restrict__ a, float* __restrict__ b)
+{
+    extern __shared__ float pad[];
+    int x0, y0, img;
+    unit(blockIdx.x, x0, y0, img);
+    const int th = min(TH, R - y0), xl = x0 + 4 * threadIdx.x;
+    const float* ap = a + img * PLANE + xl;
+    float* bp = b + img * PLANE + xl;
+    constexpr int P = 4;
+    f4 pf[P];
+#pragma unroll
+    for (int u = 0; u < P; ++u) pf[u] = *reinterpret_cast<const f4*>(ap + (size_t)(y0 + u) * PITCH);
+    for (int k0 = 0; k0 < th; k0 += P) {
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+            const int k = min(k0 + u, th - 1);
+            const f4 v = pf[u];
+            pf[u] = *reinterpret_cast<const f4*>(ap + (size_t)(y0 + min(k0 + u + P, th - 1)) * PITCH);
+            __builtin_nontemporal_store(work<W>(v), reinterpret_cast<f4*>(bp + (size_t)(y0 + k) * PITCH));
+        }
+    }
+    if (threadIdx.x == 1000) pad[0] = 0;
+}
+
+constexpr int NBG = (NB + 2) / 3;   // band groups of 3
+template <int W>
+__global__ __launch_bounds__(256) void k_dec3W(const float* __restrict__ a, float* __restrict__ b)
+{
+    __shared__ f4 ring[3][2][4][64];                      // band, block parity, row, lane
+    extern __shared__ float pad[];
+    const int bid = blockIdx.x;
+    const int strip = bid % NS, tb = bid / NS, bg = tb % NBG, img = tb / NBG;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int x0 = strip * 256, xl = x0 + 4 * lane;
+    constexpr int nblk = TH / 4;                          // every band runs TH rows (clamped re-reads past R)
+    if (w == 0) {
+        const float* ap[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) ap[c] = a + img * PLANE + xl;
+        auto rowp = [&](int c, int k) {
+            const int y = min((3 * bg + c) * TH + k, R - 1);
+            return reinterpret_cast<const f4*>(a + img * PLANE + (size_t)y * PITCH + xl);
+        };
+        f4 s0[3][4], s1[3][4];
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s0[c][u] = *rowp(c, u);
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s1[c][u] = *rowp(c, 4 + u);
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) ring[c][0][u][lane] = s0[c][u];
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_s_barrier();
+        for (int t = 0; t < nblk; t += 2) {
+            // even block t: s1 holds block t+1 -> ring parity 1; refill s0 with block t+2
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) ring[c][1][u][lane] = s1[c][u];
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) s0[c][u] = *rowp(c, min(4 * (t + 2) + u, TH - 1));
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_s_barrier();
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) ring[c][0][u][lane] = s0[c][u];
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) s1[c][u] = *rowp(c, min(4 * (t + 3) + u, TH - 1));
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_s_barrier();
+        }
+    } else {
+        const int c = w - 1, band = 3 * bg + c;
+        float* bp = b + img * PLANE + xl;
+        __builtin_amdgcn_s_barrier();
+        for (int t = 0; t < nblk; ++t) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int y = min(band * TH + 4 * t + u, R - 1);
+                const f4 v = ring[c][t & 1][u][lane];
+                __builtin_nontemporal_store(work<W>(v), reinterpret_cast<f4*>(bp + (size_t)y * PITCH));
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_s_barrier();
+        }
+    }
+    if (threadIdx.x == 1000) pad[0] = 0;
+}
+
 __global__ __launch_bounds__(64) void k_loads(const float* __restrict__ a, float* __restrict__ b)
 {
     int x0, y0, img;
@@ -166,6 +281,14 @@ int main()
     rep("decoupled D=2", timeit([&] { hipLaunchKernelGGL(k_decoupled<2>, dim3(units), dim3(128), 0, 0, a, b); }), alg);
     rep("decoupled D=3", timeit([&] { hipLaunchKernelGGL(k_decoupled<3>, dim3(units), dim3(128), 0, 0, a, b); }), alg);
     rep("decoupled D=4", timeit([&] { hipLaunchKernelGGL(k_decoupled<4>, dim3(units), dim3(128), 0, 0, a, b); }), alg);
+    // blur-shaped: 2 blur waves per SIMD (8 per CU): coupled one-wave units with 20 KB of LDS
+    // each; decoupled 4-wave workgroups with 40 KB (2 per CU: 6 compute + 2 loader waves)
+    const int units3 = NS * NBG * NIMG;
+    const double alg3 = 2.0 * (double)NIMG * NBG * 3 * TH * 2560 * 4;
+    rep("coupledW8 occ2", timeit([&] { hipLaunchKernelGGL(k_coupledW<8>, dim3(units), dim3(64), 20480, 0, a, b); }), alg);
+    rep("dec3W8 occ2", timeit([&] { hipLaunchKernelGGL(k_dec3W<8>, dim3(units3), dim3(256), 40960 - 24576, 0, a, b); }), alg3);
+    rep("coupledW32 occ2", timeit([&] { hipLaunchKernelGGL(k_coupledW<32>, dim3(units), dim3(64), 20480, 0, a, b); }), alg);
+    rep("dec3W32 occ2", timeit([&] { hipLaunchKernelGGL(k_dec3W<32>, dim3(units3), dim3(256), 40960 - 24576, 0, a, b); }), alg3);
     rep("loads only", timeit([&] { hipLaunchKernelGGL(k_loads, dim3(units), dim3(64), 0, 0, a, b); }), alg / 2);
     rep("stores only", timeit([&] { hipLaunchKernelGGL(k_stores, dim3(units), dim3(64), 0, 0, a, b); }), alg / 2);
     // correctness of the copies: b = 2 a

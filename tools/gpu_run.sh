@@ -2,7 +2,7 @@
 # One evidence pass on a GPU box (run through gpurun from the repo root):
 #   bash tools/gpu_run.sh <outdir> [steps...]
 # steps (default: tests smoke bench): tests | smoke | bench | distbench | kprof | seqprof | attr | probe:<tools binary>
-#   | gpuonly:<pytest -k expr>
+#   | gpuonly:<pytest -k expr> | ab:<variant>[,<variant>...] (tools/variants/<name>/libvo.so)
 # Every GPU step has its own time limit and the chain stops at the first failure.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -39,6 +39,9 @@ for st in $STEPS; do
   probe:*)
     b=${st#probe:}; timeout -k 10 120 ./tools/$b > $O/$b.txt 2>&1 || { cat $O/$b.txt; exit 1; }
     cat $O/$b.txt ;;
+  ab:*)
+    v=${st#ab:}; timeout -k 10 900 bash tools/variant_bench.sh ${v//,/ } > $O/ab_${v//,/_}.txt 2>&1 || { cat $O/ab_${v//,/_}.txt; exit 1; }
+    cat $O/ab_${v//,/_}.txt ;;
   attr)
     timeout -k 10 400 python3 tools/fullpath_attr.py 1024 64 > $O/fullpath_attr.json 2> $O/fullpath_attr.err || { tail -20 $O/fullpath_attr.err; exit 1; }
     python3 -c "import json;d=json.load(open('$O/fullpath_attr.json'));print('attr',d['ms_per_batch'])" ;;
