@@ -147,7 +147,11 @@ VO_HD float vo_atan2_deg(float y, float x)
     const int red = lo > 0.41421356f * hi;
     const float num = red ? lo - hi : lo;
     const float den = red ? lo + hi : hi;
+#ifdef VO_TIMING_ATAN2_DIV   /* timing experiment only (libvo variant builds): the IEEE division */
+    const float t = num / (den > 1e-30f ? den : 1e-30f);
+#else
     const float t = num * vo_rcp_nr(den > 1e-30f ? den : 1e-30f);
+#endif
     const float t2 = t * t;
     /* odd Taylor series to t^15, |t| <= tan(pi/8) -> truncation < 2e-8 */
     float p = -1.0f / 15.0f;

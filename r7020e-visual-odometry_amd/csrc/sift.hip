@@ -1542,7 +1542,11 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
             for (int q = 0; q < U; ++q) {
                 const float dx = gx[q], dy = gy[q];
                 const int ai = abs(ii[q]), aj = abs(jj[q]);
+#if VO_TIMING_WEXP   // timing experiment only (not the spec)
+                const float w = vo_expf_nonpos((float)(ai * ai + aj * aj) * expf_scale);
+#else
                 const float w = tab ? wtab[ai] * wtab[aj] : vo_sift_wt(expf_scale, ai) * vo_sift_wt(expf_scale, aj);
+#endif
                 float mag = vo_grad_mag(dx, dy);
                 float ori = vo_atan2_deg(dy, dx);
                 int bin = vo_round((float)VO_SIFT_ORI_BINS / 360.0f * ori);   // ori in [0, 360): bin in [0, 36]
@@ -1890,8 +1894,14 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
                 for (int u = 0; u < U; ++u) {
                     if (sb + 64 * u + lane < nsamp) {
                         const float fi = (float)S[u].i, fj = (float)S[u].j;
+#if VO_TIMING_WEXP   // timing experiment only (not the spec): one exp of the combined argument per sample
+                        const float cr_ = fj * cos_t - fi * sin_t, rr_ = fj * sin_t + fi * cos_t;
+                        accum(cr_, rr_, vo_expf_nonpos((cr_ * cr_ + rr_ * rr_) * exp_scale), S[u].g[0] - S[u].g[1],
+                              S[u].g[2] - S[u].g[3]);
+#else
                         accum(fj * cos_t - fi * sin_t, fj * sin_t + fi * cos_t, wtab[abs(S[u].i)] * wtab[abs(S[u].j)],
                               S[u].g[0] - S[u].g[1], S[u].g[2] - S[u].g[3]);
+#endif
                     }
                 }
             };
