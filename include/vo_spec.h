@@ -116,16 +116,17 @@ VO_HD float vo_rcp_nr(float d)
 }
 
 /* ------------------------------------------------------------------------ */
-/* SIFT window weights, separable.  OpenCV weighs an orientation sample by   */
-/* exp((i^2 + j^2) s) and a descriptor sample by exp((c_rot^2 + r_rot^2) s)  */
-/* with c_rot^2 + r_rot^2 = (i^2 + j^2) / hist_width^2 (a rotation).  The    */
-/* spec takes the product of the two one-dimensional factors,                */
-/*   w(i, j) = vo_sift_wt(s, |i|) * vo_sift_wt(s, |j|),                      */
+/* Descriptor window weight, separable.  OpenCV weighs a descriptor sample  */
+/* by exp((c_rot^2 + r_rot^2) s) with c_rot^2 + r_rot^2 = (i^2 + j^2) /      */
+/* hist_width^2 (a rotation).  The spec takes the product of the two         */
+/* one-dimensional factors (s' = s / hist_width^2),                          */
+/*   w(i, j) = vo_sift_wt(s', |i|) * vo_sift_wt(s', |j|),                    */
 /* equal in exact arithmetic and within float rounding of OpenCV's value,    */
-/* so the kernels read both factors from a per-keypoint table of radius + 1  */
-/* entries instead of evaluating an exp per sample.  k^2 s must lie in       */
-/* [-87, 0] (vo_expf_nonpos): at most ~5 for the orientation window, ~1.6    */
-/* for the descriptor's rotated square.                                      */
+/* so k_desc reads both factors from a per-keypoint table of radius + 1      */
+/* entries instead of evaluating an exp per sample.  k^2 s' must lie in      */
+/* [-87, 0] (vo_expf_nonpos): at most ~1.6 over the rotated square.  (The    */
+/* orientation window keeps one exp of (i^2 + j^2) s: there the table's two  */
+/* LDS reads per sample measured slower than the exp)        */
 /* ------------------------------------------------------------------------ */
 VO_HD float vo_sift_wt(float s, int k) { return vo_expf_nonpos((float)(k * k) * s); }
 
@@ -147,11 +148,7 @@ VO_HD float vo_atan2_deg(float y, float x)
     const int red = lo > 0.41421356f * hi;
     const float num = red ? lo - hi : lo;
     const float den = red ? lo + hi : hi;
-#ifdef VO_TIMING_ATAN2_DIV   /* timing experiment only (libvo variant builds): the IEEE division */
-    const float t = num / (den > 1e-30f ? den : 1e-30f);
-#else
     const float t = num * vo_rcp_nr(den > 1e-30f ? den : 1e-30f);
-#endif
     const float t2 = t * t;
     /* odd Taylor series to t^15, |t| <= tan(pi/8) -> truncation < 2e-8 */
     float p = -1.0f / 15.0f;

@@ -293,9 +293,6 @@ static int orientations(const float* img, int rows, int cols, int r, int c, floa
 #else
     uint64_t hfx[VO_SIFT_ORI_BINS];
     memset(hfx, 0, sizeof(hfx));
-    /* separable window weight (vo_spec.h vo_sift_wt): w(i, j) = wt[|i|] * wt[|j|] */
-    float* wt = (float*)malloc(sizeof(float) * (size_t)(radius + 1));
-    for (int k = 0; k <= radius; ++k) wt[k] = vo_sift_wt(expf_scale, k);
 #endif
     for (int i = -radius; i <= radius; ++i) {
         int y = r + i;
@@ -305,11 +302,7 @@ static int orientations(const float* img, int rows, int cols, int r, int c, floa
             if (x <= 0 || x >= cols - 1) continue;
             float dx = AT(img, cols, y, x + 1) - AT(img, cols, y, x - 1);
             float dy = AT(img, cols, y - 1, x) - AT(img, cols, y + 1, x);
-#ifdef VO_CV_LITERAL
             float w = SIFT_EXPF((float)(i * i + j * j) * expf_scale);
-#else
-            float w = wt[i < 0 ? -i : i] * wt[j < 0 ? -j : j];
-#endif
             float mag = sqrtf(dx * dx + dy * dy);
             float ori = SIFT_ATAN2(dy, dx);
             int bin = vo_round((float)n / 360.0f * ori);
@@ -326,7 +319,6 @@ static int orientations(const float* img, int rows, int cols, int r, int c, floa
 #ifdef VO_CV_LITERAL
     for (int k = 0; k < n; ++k) t[k] = hfl[k];
 #else
-    free(wt);
     for (int k = 0; k < n; ++k) t[k] = vo_hist_fx_to_float(hfx[k]);
 #endif
     float maxval = 0.0f;

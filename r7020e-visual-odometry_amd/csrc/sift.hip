@@ -1481,10 +1481,6 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
     __shared__ __attribute__((aligned(16))) uint32_t hp[HS * NC];
     __shared__ float tf[VO_SIFT_ORI_BINS];
     __shared__ float hs[VO_SIFT_ORI_BINS];
-    // separable window weights (vo_spec.h vo_sift_wt) for radii up to OWT; larger windows (sigma
-    // far above the default) evaluate the same factors inline -- the same bits either way
-    constexpr int OWT = 64;
-    __shared__ float wtab[OWT + 1];
     const int lane = threadIdx.x;
     __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
     const long total = flat_setup(n_cand, cand_cap, n_img, fpre);
@@ -1503,9 +1499,6 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
         const int radius = vo_round(VO_SIFT_ORI_RADIUS * scl);
         const float sigw = VO_SIFT_ORI_SIG * scl;
         const float expf_scale = -1.0f / (2.0f * sigw * sigw);
-        const bool tab = radius <= OWT;                    // wave-uniform
-        if (tab)
-            for (int k2 = lane; k2 <= radius; k2 += 64) wtab[k2] = vo_sift_wt(expf_scale, k2);
         typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int b2 = 4 * lane; b2 < HS * NC; b2 += 256) *reinterpret_cast<u4_t*>(&hp[b2]) = u4_t{0u, 0u, 0u, 0u};
@@ -1541,12 +1534,11 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
 #pragma unroll
             for (int q = 0; q < U; ++q) {
                 const float dx = gx[q], dy = gy[q];
-                const int ai = abs(ii[q]), aj = abs(jj[q]);
-#if VO_TIMING_WEXP   // timing experiment only (not the spec)
-                const float w = vo_expf_nonpos((float)(ai * ai + aj * aj) * expf_scale);
-#else
-                const float w = tab ? wtab[ai] * wtab[aj] : vo_sift_wt(expf_scale, ai) * vo_sift_wt(expf_scale, aj);
-#endif
+                // one exp of the combined argument (i^2 + j^2 exact in float); a separable table
+                // (vo_sift_wt, as k_desc uses) measured slower here: 0.60 vs 0.55 ms isolated -- its
+                // two dependent LDS reads per sample cost more than the exp (profiles/r04_d_*)
+                const float fi = (float)ii[q], fj = (float)jj[q];
+                const float w = vo_expf_nonpos((fi * fi + fj * fj) * expf_scale);   // arg in [-21, 0]
                 float mag = vo_grad_mag(dx, dy);
                 float ori = vo_atan2_deg(dy, dx);
                 int bin = vo_round((float)VO_SIFT_ORI_BINS / 360.0f * ori);   // ori in [0, 360): bin in [0, 36]
@@ -1894,14 +1886,8 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
                 for (int u = 0; u < U; ++u) {
                     if (sb + 64 * u + lane < nsamp) {
                         const float fi = (float)S[u].i, fj = (float)S[u].j;
-#if VO_TIMING_WEXP   // timing experiment only (not the spec): one exp of the combined argument per sample
-                        const float cr_ = fj * cos_t - fi * sin_t, rr_ = fj * sin_t + fi * cos_t;
-                        accum(cr_, rr_, vo_expf_nonpos((cr_ * cr_ + rr_ * rr_) * exp_scale), S[u].g[0] - S[u].g[1],
-                              S[u].g[2] - S[u].g[3]);
-#else
                         accum(fj * cos_t - fi * sin_t, fj * sin_t + fi * cos_t, wtab[abs(S[u].i)] * wtab[abs(S[u].j)],
                               S[u].g[0] - S[u].g[1], S[u].g[2] - S[u].g[3]);
-#endif
                     }
                 }
             };

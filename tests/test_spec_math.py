@@ -35,10 +35,11 @@ def test_rcp_nr_accuracy(oracle):
 
 
 def test_sift_wt_is_the_separable_window_weight(oracle):
-    """vo_sift_wt(s, |i|) * vo_sift_wt(s, |j|) (the k_orient / k_desc window weight) agrees with
-    OpenCV's exp((i^2 + j^2) s) to float rounding over the windows' argument range."""
-    s = np.float32(-1.0 / (2.0 * (1.5 * 3.2) ** 2))
-    k = np.arange(0, 15)
+    """vo_sift_wt(s, |i|) * vo_sift_wt(s, |j|) (the k_desc window weight, s = -1/8 / hist_width^2)
+    agrees with OpenCV's exp((i^2 + j^2) s) to float rounding over the descriptor window."""
+    hw = np.float32(3.0 * 3.2)
+    s = np.float32(np.float32(-0.125) / (hw * hw))
+    k = np.arange(0, 35)
     wk = oracle.spec_eval("sift_wt", np.stack([np.full(len(k), s, np.float64), k], 1).reshape(-1))
     i, j = np.meshgrid(k, k)
     w = (wk[i].astype(np.float32) * wk[j].astype(np.float32)).astype(np.float64)

@@ -2,7 +2,7 @@
 # One evidence pass on a GPU box (run through gpurun from the repo root):
 #   bash tools/gpu_run.sh <outdir> [steps...]
 # steps (default: tests smoke bench): tests | smoke | bench | distbench | kprof | seqprof | attr | probe:<tools binary>
-#   | gpuonly:<pytest -k expr> | ab:<variant>[,<variant>...] (tools/variants/<name>/libvo.so)
+#   | gpuonly:<pytest -k expr, + for spaces> | ab:<variant>[,<variant>...] (tools/variants/<name>/libvo.so)
 # Every GPU step has its own time limit and the chain stops at the first failure.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -15,7 +15,7 @@ for st in $STEPS; do
       || { tail -40 $O/gpu_tests.log; exit 1; }
     tail -1 $O/gpu_tests.log ;;
   gpuonly:*)
-    timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -k "${st#gpuonly:}" > $O/gpu_sel.log 2>&1 \
+    k=${st#gpuonly:}; timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -k "${k//+/ }" > $O/gpu_sel.log 2>&1 \
       || { tail -40 $O/gpu_sel.log; exit 1; }
     tail -1 $O/gpu_sel.log ;;
   smoke)
