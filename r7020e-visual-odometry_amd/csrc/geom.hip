@@ -13,9 +13,10 @@
 //       stops; msac_final: inlier mask + camera pose.  (The eager kernels
 //       k_msac_hyp / k_msac_score / k_msac_select score every slot first; they
 //       are compiled only into the test build libvo_exp.so, VO_EXPERIMENTAL.)
-//   landmarks (VO.m:145-160, CreateLandmarksFromFeatures.m)  k_lm_frame: one
-//       block per frame -- stereo positions, the any-x-or-y equality filter
-//       (quirk Q3) + block compaction, odd-row DLT with the z gates.  The world transform needs the chained pose and runs
+//   landmarks (VO.m:145-160, CreateLandmarksFromFeatures.m)  k_stereo_pos,
+//       k_lm_filter (any-x-or-y equality test, quirk Q3) + block compaction,
+//       k_lm_tri (odd rows, z gates).  (One fused block per frame measured
+//       3.5x slower: 0.27 vs 0.075 ms per batch for positions + filter.)  The world transform needs the chained pose and runs
 //       on the host after the 4x4 chain.
 // Float/double expressions mirror oracle/vo_ref.c operation for operation.
 #include "vo_geom.h"
@@ -694,6 +695,23 @@ __global__ __launch_bounds__(VO_MSAC_T) void k_msac(MsacArgs a)
 // ---------------------------------------------------------------------------
 // landmarks
 // ---------------------------------------------------------------------------
+// stereo subset positions of frame f (VO.m:141-142): spos[f][j] = (lx, ly, rx, ry)
+__global__ void k_stereo_pos(const vo_keypoint* __restrict__ kp, int kp_cap, const int* __restrict__ pair_i,
+                             const int* __restrict__ pair_j, const int* __restrict__ pair_n, float* __restrict__ spos,
+                             int* __restrict__ s_n)
+{
+    const int f = blockIdx.y, K = kp_cap;
+    int n = pair_n[f];
+    if (n > K) n = K;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        const vo_keypoint l = kp[(size_t)(2 * f) * K + pair_i[(size_t)f * K + j]];
+        const vo_keypoint r = kp[(size_t)(2 * f + 1) * K + pair_j[(size_t)f * K + j]];
+        float* p = spos + ((size_t)f * K + j) * 4;
+        p[0] = l.x; p[1] = l.y; p[2] = r.x; p[3] = r.y;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) s_n[f] = n;
+}
+
 __device__ __forceinline__ uint32_t block_exscan_1024_g(uint32_t v, uint32_t* sh, uint32_t* total)
 {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -721,50 +739,31 @@ __device__ __forceinline__ uint32_t block_exscan_1024_g(uint32_t v, uint32_t* sh
     return before + x - v;
 }
 
-// The landmark half of the loop body for one frame, one 1024-thread block per frame (was three
-// launches: stereo positions, filter, triangulation -- each a short chain of single-block-per-frame
-// work that, in the pipelined loop, waited for wave slots behind the next batch's scale space):
-//  1. FROM_KP: stereo subset positions (VO.m:141-142) spos[f][j] = (lx, ly, rx, ry) of the stereo
-//     pairs, s_n[f] = S (without FROM_KP, vo_landmarks' host-provided spos / s_n are used);
-//  2. new-landmark filter (VO.m:147-154) + compaction: stereo matches 1024 at a time (one per
-//     thread, rounds keep the ascending order of the compaction), the old points staged through
-//     LDS 1024 at a time and compared against every match (broadcast reads); hit = any old left x
-//     == lx or any old left y == ly, or likewise on the right (VO.m:150-151, exact equality);
-//     flags go to lm_keep as byte scratch, the new indices to lm_new, their count to lm_M;
-//  3. CreateLandmarksFromFeatures.m:2-16: odd 1-based rows (even 0-based) triangulated (f64 DLT),
-//     z gates, lm_X / lm_keep rows, lm_rows = max(2, last kept row + 1) (zeros(.., 2) floor).
+// new-landmark filter (VO.m:147-154) + compaction.  one block (1024) per frame.
 // old positions: oldpos[f][k] (x1, y1, x2, y2) for k < *kn (kn[f * kn_stride]).
-template <bool FROM_KP>
-__global__ __launch_bounds__(1024) void k_lm_frame(const vo_keypoint* __restrict__ kp, const int* __restrict__ pair_i,
-                                                   const int* __restrict__ pair_j, const int* __restrict__ pair_n,
-                                                   float* __restrict__ spos, int* __restrict__ s_n,
-                                                   const float* __restrict__ oldpos, const int* __restrict__ kn,
-                                                   int kn_stride, int kp_cap, uint8_t* __restrict__ lm_keep,
-                                                   int* __restrict__ lm_new, int* __restrict__ lm_M, int* __restrict__ lm_rows)
+// flags: per-frame byte scratch (lm_keep, rewritten later by k_lm_tri).
+__global__ __launch_bounds__(1024) void k_lm_filter(const float* __restrict__ spos, const int* __restrict__ s_n,
+                                                    const float* __restrict__ oldpos, const int* __restrict__ kn,
+                                                    int kn_stride, int kp_cap, uint8_t* __restrict__ flags,
+                                                    int* __restrict__ lm_new, int* __restrict__ lm_M,
+                                                    int* __restrict__ lm_rows)
 {
+    // One block per frame.  Stereo matches are taken 1024 at a time (one per thread,
+    // rounds keep the ascending order of the compaction); the old points are staged
+    // through LDS 1024 at a time and every thread compares its match against all of
+    // them (broadcast reads).  hit = any old left x == lx or any old left y == ly, or
+    // likewise on the right (VO.m:150-151, exact float equality).
     __shared__ uint32_t sh[32];
     __shared__ float4 so[1024];
     const int f = blockIdx.x, tid = threadIdx.x, K = kp_cap;
-    float4* const sp = reinterpret_cast<float4*>(spos + (size_t)f * K * 4);
-    int S;
-    if constexpr (FROM_KP) {
-        S = min(pair_n[f], K);
-        for (int j = tid; j < S; j += 1024) {
-            const vo_keypoint l = kp[(size_t)(2 * f) * K + pair_i[(size_t)f * K + j]];
-            const vo_keypoint r = kp[(size_t)(2 * f + 1) * K + pair_j[(size_t)f * K + j]];
-            sp[j] = float4{l.x, l.y, r.x, r.y};
-        }
-        if (tid == 0) s_n[f] = S;
-        __syncthreads();                                    // spos rows of other threads below
-    } else {
-        S = min(s_n[f], K);
-    }
+    int S = s_n[f];
+    if (S > K) S = K;
     int nk = kn[(size_t)f * kn_stride];
     if (nk > K) nk = K;
     if (nk < 0) nk = 0;
+    const float4* sp = reinterpret_cast<const float4*>(spos + (size_t)f * K * 4);
     const float4* op = reinterpret_cast<const float4*>(oldpos + (size_t)f * K * 4);
-    uint8_t* fl = lm_keep + (size_t)f * K;
-    int* const nw = lm_new + (size_t)f * K;
+    uint8_t* fl = flags + (size_t)f * K;
     uint32_t done = 0;                                      // new landmarks emitted by earlier rounds
     for (int j0 = 0; j0 < S; j0 += 1024) {
         const int j = j0 + tid;
@@ -796,9 +795,10 @@ __global__ __launch_bounds__(1024) void k_lm_frame(const vo_keypoint* __restrict
         if (valid) fl[j] = (uint8_t)isnew;
         uint32_t total;
         const uint32_t pos = block_exscan_1024_g(isnew, sh, &total);
-        if (isnew) nw[done + pos] = j;
+        if (isnew) lm_new[(size_t)f * K + done + pos] = j;
         done += total;
     }
+    __syncthreads();
     if (tid == 0) {
         lm_M[f] = (int)done;
         lm_rows[f] = 2;                                     // zeros(size(features_l,2),3): 2 rows
@@ -806,10 +806,7 @@ __global__ __launch_bounds__(1024) void k_lm_frame(const vo_keypoint* __restrict
     }
 }
 
-// CreateLandmarksFromFeatures.m:2-16: odd 1-based rows (even 0-based), triangulate (f64 DLT), z
-// gates, lm_rows = max(2, last kept row + 1).  16 blocks of 64 per frame: the f64 Jacobi SVD per
-// point is the heavy part, so it is spread over CUs (inside k_lm_frame's one block per frame it
-// took 0.32 ms per 64-frame batch against 0.06 here).
+// CreateLandmarksFromFeatures: odd 1-based rows (even 0-based), triangulate, z gates.
 __global__ void k_lm_tri(const float* __restrict__ spos, const int* __restrict__ lm_new, const int* __restrict__ lm_M,
                          int kp_cap, CalibDev cal, float* __restrict__ lm_X, uint8_t* __restrict__ lm_keep,
                          int* __restrict__ lm_rows)
@@ -899,8 +896,9 @@ void geom_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_trac
     VO_LAUNCH(k_gather_tri, dim3(16, B), dim3(64), 0, s, a.sb->kp, K, g.lists, g.list_n, g.oldpos, g.imgpt, g.world, M, cal);
     MsacArgs ma = msac_args(g, g.imgpt, g.world, g.list_n + 3, 4, a.calib.K, a.rp, (uint32_t)a.frame_index0);
     msac_enqueue(ma, B, s);
-    VO_LAUNCH_NAMED("k_lm_frame", k_lm_frame<true>, dim3(B), dim3(1024), 0, s, a.sb->kp, a.pair_i, a.pair_j, a.pair_n, g.spos, g.s_n,
-              g.oldpos, g.list_n + 3, 4, K, g.lm_keep, g.lm_new, g.lm_M, g.lm_rows);
+    VO_LAUNCH(k_stereo_pos, dim3(16, B), dim3(256), 0, s, a.sb->kp, K, a.pair_i, a.pair_j, a.pair_n, g.spos, g.s_n);
+    VO_LAUNCH(k_lm_filter, dim3(B), dim3(1024), 0, s, g.spos, g.s_n, g.oldpos, g.list_n + 3, 4, K, g.lm_keep, g.lm_new,
+              g.lm_M, g.lm_rows);
     VO_LAUNCH(k_lm_tri, dim3(16, B), dim3(64), 0, s, g.spos, g.lm_new, g.lm_M, K, cal, g.lm_X, g.lm_keep, g.lm_rows);
 }
 
@@ -948,8 +946,8 @@ void estworldpose_launch(GeomBuffers& g, const double* img, const double* world,
 void landmarks_launch(GeomBuffers& g, const int* kn, const vo_calib& c, hipStream_t s)
 {
     CalibDev cal = calib_dev(c);
-    VO_LAUNCH_NAMED("k_lm_frame", k_lm_frame<false>, dim3(1), dim3(1024), 0, s, nullptr, nullptr, nullptr, nullptr, g.spos, g.s_n, g.oldpos, kn,
-              0, g.kp_cap, g.lm_keep, g.lm_new, g.lm_M, g.lm_rows);
+    VO_LAUNCH(k_lm_filter, dim3(1), dim3(1024), 0, s, g.spos, g.s_n, g.oldpos, kn, 0, g.kp_cap, g.lm_keep, g.lm_new, g.lm_M,
+              g.lm_rows);
     VO_LAUNCH(k_lm_tri, dim3(16, 1), dim3(64), 0, s, g.spos, g.lm_new, g.lm_M, g.kp_cap, cal, g.lm_X, g.lm_keep, g.lm_rows);
 }
 

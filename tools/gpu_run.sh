@@ -1,7 +1,7 @@
 #!/bin/bash
 # One evidence pass on a GPU box (run through gpurun from the repo root):
 #   bash tools/gpu_run.sh <outdir> [steps...]
-# steps (default: tests smoke bench): tests | smoke | bench | distbench | kprof | seqprof | attr | probe:<tools binary>
+# steps (default: tests smoke bench): tests | smoke | bench | distbench | kprof | seqprof | pmc | attr | probe:<tools binary>
 #   | gpuonly:<pytest -k expr, + for spaces> | ab:<variant>[,<variant>...] (tools/variants/<name>/libvo.so)
 # Every GPU step has its own time limit and the chain stops at the first failure.
 set -e
@@ -42,6 +42,9 @@ for st in $STEPS; do
   ab:*)
     v=${st#ab:}; timeout -k 10 900 bash tools/variant_bench.sh ${v//,/ } > $O/ab_${v//,/_}.txt 2>&1 || { cat $O/ab_${v//,/_}.txt; exit 1; }
     cat $O/ab_${v//,/_}.txt ;;
+  pmc)
+    timeout -k 10 900 bash tools/pmc_passes.sh _$(basename $O) > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
+    echo pmc-done ;;
   attr)
     timeout -k 10 400 python3 tools/fullpath_attr.py 1024 64 > $O/fullpath_attr.json 2> $O/fullpath_attr.err || { tail -20 $O/fullpath_attr.err; exit 1; }
     python3 -c "import json;d=json.load(open('$O/fullpath_attr.json'));print('attr',d['ms_per_batch'])" ;;
