@@ -197,6 +197,11 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
+    # stdout carries exactly the one JSON line: native libraries' chatter on fd 1 (RCCL prints its
+    # version banner at communicator creation) goes to stderr; the line goes to a saved copy
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
     import vo_amd  # noqa: F401
     from r7020e_visual_odometry_amd import vo, synthetic as syn, roofline
@@ -215,7 +220,7 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         if rank == 0:
-            print(json.dumps({"dry_run": True, "n_gpus": world}))
+            print(json.dumps({"dry_run": True, "n_gpus": world}), file=json_out, flush=True)
         return
     # VO_BENCH_FORCE_DIST=1: take the process-group branch (RCCL with the default backend) even
     # at one rank -- the only way this pool can run the collectives on hardware before an
@@ -457,7 +462,7 @@ def main():
             "full_path": full,
             "large": large,
         }
-        print(json.dumps(line))
+        print(json.dumps(line), file=json_out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
     ctx.close()

@@ -27,7 +27,7 @@ for st in $STEPS; do
   distbench)
     VO_BENCH_FORCE_DIST=1 timeout -k 10 600 python3 bench.py --no-cpu --large-batch 0 > $O/distbench.json 2> $O/distbench.err \
       || { tail -20 $O/distbench.err; exit 1; }
-    python3 -c "import json;d=json.load(open('$O/distbench.json'));f=d['full_path'];print('distbench',d['config']['process_group'],round(d['value']),'full',round(f['value']),f['landmark_rows'],f['accuracy']['ate_rmse_m'])" ;;
+    python3 -c "import json;d=json.loads([l for l in open('$O/distbench.json') if l.startswith('{')][0]);f=d['full_path'];print('distbench',d['config']['process_group'],round(d['value']),'full',round(f['value']),f['landmark_rows'],f['accuracy']['ate_rmse_m'])" ;;
   kprof)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kprof -o k -- python3 bench.py --steps 10 --runs 1 --warmup 2 --no-cpu --seq-frames 0 --large-batch 0 > $O/kprof_bench.json 2> $O/kprof.err
     find $O/kprof -name "*kernel_trace.csv" -delete
