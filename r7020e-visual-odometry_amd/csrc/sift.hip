@@ -2190,7 +2190,10 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
 // 32768 one-wave workgroups (~7 keypoints each at 64 frames x ~1.8k): shorter tail than
 // 8192 (k_desc 2.25 -> 2.05 ms, k_orient 0.77 -> 0.67 ms isolated) and workgroups turn over
 // often enough for the scale-space stream's blurs to get slots while they run
-constexpr int kFeatureGrid = 32768;
+#ifndef VO_FEATURE_GRID
+#define VO_FEATURE_GRID 32768
+#endif
+constexpr int kFeatureGrid = VO_FEATURE_GRID;
 
 // The extremum test of octaves [o_begin, o_end).  vo_api.hip enqueues it in two parts on the
 // feature stream: octave 0 as soon as the scale-space stream records ev_o0 (beside the level blurs

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One evidence pass on a GPU box (run through gpurun from the repo root):
 #   bash tools/gpu_run.sh <outdir> [steps...]
-# steps (default: tests smoke bench): tests | smoke | bench | distbench | kprof | seqprof | pmc | attr | probe:<tools binary>
+# steps (default: tests smoke bench): tests | smoke | bench | distbench | kprof | seqprof | pmc | attr | batch:<B> | probe:<tools binary>
 #   | gpuonly:<pytest -k expr, + for spaces> | ab:<variant>[,<variant>...] (tools/variants/<name>/libvo.so)
 # Every GPU step has its own time limit and the chain stops at the first failure.
 set -e
@@ -45,6 +45,12 @@ for st in $STEPS; do
   pmc)
     timeout -k 10 900 bash tools/pmc_passes.sh _$(basename $O) > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
     echo pmc-done ;;
+  batch:*)
+    b=${st#batch:}
+    for bb in 64 $b 64; do
+      timeout -k 10 300 python3 bench.py --no-cpu --seq-frames 0 --large-batch 0 --batch $bb > $O/batch_$bb.json 2>/dev/null || { echo "batch $bb failed"; exit 1; }
+      python3 -c "import json;d=json.load(open('$O/batch_$bb.json'));print('batch',$bb,round(d['value'],1),round(d['ms_per_step'],3))"
+    done ;;
   attr)
     timeout -k 10 400 python3 tools/fullpath_attr.py 1024 64 > $O/fullpath_attr.json 2> $O/fullpath_attr.err || { tail -20 $O/fullpath_attr.err; exit 1; }
     python3 -c "import json;d=json.load(open('$O/fullpath_attr.json'));print('attr',d['ms_per_batch'])" ;;
