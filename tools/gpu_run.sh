@@ -2,7 +2,7 @@
 # One evidence pass on a GPU box (run through gpurun from the repo root):
 #   bash tools/gpu_run.sh <outdir> [steps...]
 # steps (default: tests smoke bench): tests | smoke | bench | distbench | kprof | seqprof | pmc | attr | batch:<B> | probe:<tools binary>
-#   | gpuonly:<pytest -k expr, + for spaces> | ab:<variant>[,<variant>...] (tools/variants/<name>/libvo.so)
+#   | gpuonly:<pytest -k expr, + for spaces> | vtests:<variant>:<expr> | ab:<variant>[,<variant>...] (tools/variants/<name>/libvo.so)
 # Every GPU step has its own time limit and the chain stops at the first failure.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -18,6 +18,12 @@ for st in $STEPS; do
     k=${st#gpuonly:}; timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -k "${k//+/ }" > $O/gpu_sel.log 2>&1 \
       || { tail -40 $O/gpu_sel.log; exit 1; }
     tail -1 $O/gpu_sel.log ;;
+  vtests:*)
+    # vtests:<variant>:<pytest -k expr, + for spaces> — GPU tests against tools/variants/<variant>/libvo.so
+    a=${st#vtests:}; v=${a%%:*}; k=${a#*:}
+    VO_LIBPATH=$PWD/tools/variants/$v/libvo.so timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "${k//+/ }" > $O/vtests_$v.log 2>&1 \
+      || { tail -40 $O/vtests_$v.log; exit 1; }
+    tail -1 $O/vtests_$v.log ;;
   smoke)
     timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
     tail -1 $O/smoke.log ;;
