@@ -828,195 +828,6 @@ __global__ __launch_bounds__(64, (RAD <= VO_BLUR_OCC3_MAXR || CPL == 2) ? 3 : 2)
         blur_stream_body<RAD, false, TAG, CPL>(src + os, pitch, R, C, g_out + od, K, x0, y0, THb, rb, u8, nbo, stg);
 }
 
-// ---------------------------------------------------------------------------
-// Octave-0 level cascade (VO_OCT0_CASCADE): levels 1..5 of octave 0 in one launch.  One workgroup
-// per (strip, image) with one wave per level; the waves run in lockstep, one s_barrier per row step,
-// and hand rows down the cascade through double-buffered LDS row slots, so G1..G4 are written to
-// HBM once and never re-read (the per-level kernels read each level back: 16 B per octave-0 pixel).
-// Each wave keeps its level's row-pass ring in registers (as k_blur_stream does) and computes its
-// level on the reflect-101-extended domain: a strip spans 256 lane columns of which the middle
-// kCasSW are valid for every level (the cumulative radius 42 <= kCasH each side), and level i runs
-// over rows -E_{i+1} .. R-1+E_{i+1} (E_i = sum of the radii of levels >= i), level 1 from reflected
-// G0 rows.  Extended values equal the reflected plane values bit for bit: every tap adds the
-// symmetric pair s[-j] + s[+j], whose operands only swap under a reflection (float addition is
-// commutative), so no plane needs a reflection table beyond G0's.
-// Wave w (level w+1) consumes its k-th input row at step d_w + k (d_{w+1} = d_w + 2 r_{w+1} + 1: the
-// row wave w-1 wrote one step earlier), runs n_w steps, and idles through the others.
-// ---------------------------------------------------------------------------
-constexpr int kCasH = 44;                    // cumulative halo (>= 5+6+8+10+13 = 42), multiple of 4
-constexpr int kCasSW = 256 - 2 * kCasH;      // valid output columns per strip (168)
-constexpr int kCasPad = 16;                  // LDS row pad each side (>= the largest halo RH)
-constexpr int kCasRow = 256 + 2 * kCasPad;   // floats per LDS row slot
-struct CascArgs {
-    const float* g0;                         // octave 0, level 0 (image 0)
-    float* g[5];                             // levels 1..5 (image 0)
-    size_t istride;                          // floats per image
-    int R, C, pitch, n_strips, T;
-    int d[5], n[5], E[6];                    // start step, steps, E[w] = sum of radii of levels >= w+1
-    Kern K[5];
-};
-
-__device__ __forceinline__ void cas_bar()
-{
-    // LDS writes of this step complete, then the workgroup barrier; no vmcnt wait (wave 0's row
-    // prefetches stay in flight), and the clobber keeps LDS accesses on their side of it
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-template <int RAD, int W, bool EDGE = false>
-__device__ __forceinline__ void cas_level(const CascArgs& a, int img, int xw, float* __restrict__ slots)
-{
-    typedef float vec_t __attribute__((ext_vector_type(4)));
-    constexpr int P = BS_P, RH = bs_rh(RAD, 4), NQ = 1 + 2 * RH / 4, NP = 2, NR = 2 * RAD + P;
-    constexpr bool FIRST = W == 0;
-    const int lane = threadIdx.x & 63;
-    const int R = a.R, C = a.C, pitch = a.pitch;
-    const int d = a.d[W], nst = a.n[W], T = a.T;
-    const int E0 = a.E[W], E1 = a.E[W + 1];                // input rows start at -E0, outputs at -E1
-    float k[RAD + 1];
-#pragma unroll
-    for (int j = 0; j <= RAD; ++j) k[j] = a.K[W].k[j];
-    const int xl = xw + 4 * lane;
-    // output lanes: the strip's valid columns [xw + kCasH, xw + kCasH + kCasSW) inside the plane
-    const bool lane_out = lane >= kCasH / 4 && lane < (kCasH + kCasSW) / 4 && xl < C;
-    float* const gout = a.g[W] + (size_t)img * a.istride;
-    const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(gout, 0, R * pitch * 4, 0x00020000);
-    const Kern& KL = a.K[W];
-    float* const nbo = KL.nb ? KL.nb + (size_t)img * a.istride : nullptr;
-    const __amdgpu_buffer_rsrc_t rs_nb =
-        __builtin_amdgcn_make_buffer_rsrc(nbo, 0, nbo ? KL.nb_rows * KL.nb_pitch * 4 : 0, 0x00020000);
-    float* const in_slot = slots + (size_t)W * 2 * kCasRow;          // level W rows (W = 0: G0)
-    float* const out_slot = slots + (size_t)(W + 1) * 2 * kCasRow;   // level W+1 rows (W < 4)
-
-    // wave 0: G0 rows from HBM, reflected (one fold: E0 + P < R), prefetched P steps ahead
-    const float* const g0 = a.g0 + (size_t)img * a.istride;
-    // EDGE (a template parameter, so the loads sit under no branch and the compiler's waitcnt pass
-    // keeps the prefetch counts): reflected columns gathered one by one
-    int cm[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) cm[i] = vo_reflect101(xl + i, C);
-    auto g0row = [&](int kk) {
-        int q = -E0 + min(kk, nst - 1);
-        q = q < 0 ? -q : (q >= R ? 2 * R - 2 - q : q);
-        return g0 + (size_t)q * pitch;
-    };
-    auto load_g0 = [&](int kk) {
-        const float* rp = g0row(kk);
-        vec_t v;
-        if constexpr (!EDGE) v = *reinterpret_cast<const vec_t*>(rp + xl);
-        else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = rp[cm[i]];
-        }
-        return v;
-    };
-
-    for (int t = 0; t < d; ++t) cas_bar();
-    vec_t pf[P];
-    if constexpr (FIRST) {
-#pragma unroll
-        for (int u = 0; u < P; ++u) pf[u] = load_g0(u);
-    }
-    vo_f2 H[NR][NP];
-    for (int kb = 0; kb < nst; kb += P) {
-        vo_static_for<P>([&](auto uc) {
-            constexpr int u = decltype(uc)::value;
-            const int kk = kb + u, t = d + kk;
-            const float* row = in_slot + (size_t)((FIRST ? t : t - 1) & 1) * kCasRow;
-            if constexpr (FIRST) {
-                float* wr = in_slot + (size_t)(t & 1) * kCasRow;
-                *reinterpret_cast<vec_t*>(wr + kCasPad + 4 * lane) = pf[u];
-                pf[u] = load_g0(kk + P);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own row, read back below
-            }
-            float w[4 * NQ];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const vec_t v = *reinterpret_cast<const vec_t*>(row + kCasPad - RH + 4 * lane + 4 * q);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) w[4 * q + i] = v[i];
-            }
-            // row pass on column pairs (k_blur_stream's packed form, same operation order)
-            constexpr int NW = 4 * NQ;
-            vo_f2 Ev[NW / 2], Ov[NW / 2 - 1];
-#pragma unroll
-            for (int m = 0; m < NW / 2; ++m) Ev[m] = vo_f2{w[2 * m], w[2 * m + 1]};
-#pragma unroll
-            for (int m = 0; m < NW / 2 - 1; ++m) Ov[m] = __builtin_shufflevector(Ev[m], Ev[m + 1], 1, 2);
-#pragma unroll
-            for (int c = 0; c < NP; ++c) {
-                const int x = RH + 2 * c;
-                vo_f2 acc = vo_f2{k[0], k[0]} * Ev[x / 2];
-#pragma unroll
-                for (int j = 1; j <= RAD; ++j) {
-                    const vo_f2 pa = (j & 1) ? Ov[(x - j - 1) / 2] : Ev[(x - j) / 2];
-                    const vo_f2 pb = (j & 1) ? Ov[(x + j - 1) / 2] : Ev[(x + j) / 2];
-                    acc = __builtin_elementwise_fma(vo_f2{k[j], k[j]}, pa + pb, acc);
-                }
-                H[2 * RAD + u][c] = acc;
-            }
-            if (kk >= 2 * RAD) {                                  // wave-uniform
-                vec_t g;
-#pragma unroll
-                for (int c = 0; c < NP; ++c) {
-                    vo_f2 acc = vo_f2{k[0], k[0]} * H[u + RAD][c];
-#pragma unroll
-                    for (int j = 1; j <= RAD; ++j)
-                        acc = __builtin_elementwise_fma(vo_f2{k[j], k[j]}, H[u + RAD - j][c] + H[u + RAD + j][c], acc);
-                    g[2 * c] = acc.x;
-                    g[2 * c + 1] = acc.y;
-                }
-                if constexpr (W < 4)
-                    *reinterpret_cast<vec_t*>(out_slot + (size_t)(t & 1) * kCasRow + kCasPad + 4 * lane) = g;
-                const int y = -E0 + kk - RAD;
-                const bool act = lane_out && y >= 0 && y < R;
-                constexpr uint32_t OOB = 0x80000000u;
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(vo_i4, g), rs_out,
-                                                       act ? (uint32_t)(y * pitch + xl) * 4u : OOB, 0, 2);
-                // the level-L wave stores the next octave's base: even rows, the lane's even columns
-                const int yn = y >> 1, c0 = xl >> 1;
-                const bool nact = act && !(y & 1) && yn < KL.nb_rows;
-                const float g0v = g[0], g2v = g[2];
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(g0v), rs_nb,
-                                                      nact && c0 < KL.nb_cols ? (uint32_t)(yn * KL.nb_pitch + c0) * 4u : OOB, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(g2v), rs_nb,
-                                                      nact && c0 + 1 < KL.nb_cols ? (uint32_t)(yn * KL.nb_pitch + c0 + 1) * 4u
-                                                                                : OOB, 0, 0);
-            }
-            cas_bar();
-        });
-#pragma unroll
-        for (int q = 0; q < 2 * RAD; ++q)
-#pragma unroll
-            for (int c = 0; c < NP; ++c) H[q][c] = H[q + P][c];
-    }
-    for (int t = d + nst; t < T; ++t) cas_bar();
-    (void)E1;
-}
-
-// radii of the default octave (sigma 1.6, 3 layers): 5 6 8 10 13
-__global__ __launch_bounds__(320, 1) void k_oct0_cascade(CascArgs a)
-{
-    __shared__ __attribute__((aligned(16))) float slots[5 * 2 * kCasRow];
-    vo_ss_prio();
-    const int strip = blockIdx.x % a.n_strips, img = blockIdx.x / a.n_strips;
-    const int xw = strip * kCasSW - kCasH;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // pads and never-written slot columns read as finite zeros (their lanes' outputs are discarded)
-    for (int i = threadIdx.x; i < 5 * 2 * kCasRow; i += 320) slots[i] = 0.0f;
-    __syncthreads();
-    switch (w) {
-    case 0:
-        if (xw < 0 || xw + 256 > a.C) cas_level<5, 0, true>(a, img, xw, slots);
-        else cas_level<5, 0, false>(a, img, xw, slots);
-        break;
-    case 1: cas_level<6, 1>(a, img, xw, slots); break;
-    case 2: cas_level<8, 2>(a, img, xw, slots); break;
-    case 3: cas_level<10, 3>(a, img, xw, slots); break;
-    default: cas_level<13, 4>(a, img, xw, slots); break;
-    }
-}
-
 // next octave base: G0 of octave o = G_L of octave o-1 decimated by 2.  Grid (column blocks of
 // 256, rows, images): no index divisions (the grid-stride form spent ~57 VALU per element on
 // 64-bit div/mod).
@@ -2265,14 +2076,6 @@ static int fused_octaves(const Pyramid& py)
 #endif
 }
 
-// the octave-0 cascade instantiates the default octave (3 layers, sigma 1.6: radii 5 6 8 10 13)
-static bool cascade_ok(const Pyramid& py)
-{
-    const OctGeom& g = py.oct[0];
-    return py.L == 3 && py.krad[1] == 5 && py.krad[2] == 6 && py.krad[3] == 8 && py.krad[4] == 10 && py.krad[5] == 13 &&
-           g.rows > 2 * kCasH + 2 * BS_P && g.cols >= 256;
-}
-
 // First octave from which every remaining octave fits the one-launch LDS path (k_small_pyr),
 // its reflect-table length and dynamic LDS size.
 struct SmallPlan { int o_small, rtab; size_t lds; };
@@ -2358,39 +2161,6 @@ void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src
                       A + g.g_off[0], py.istride, g.pitch, C);
         }
         base_done = false;
-#ifndef VO_OCT0_CASCADE
-#define VO_OCT0_CASCADE 0
-#endif
-        if (VO_OCT0_CASCADE && o == 0 && cascade_ok(py)) {
-            CascArgs ca;
-            memset(&ca, 0, sizeof(ca));
-            ca.g0 = A + g.g_off[0];
-            for (int i = 1; i <= 5; ++i) ca.g[i - 1] = A + g.g_off[i];
-            ca.istride = py.istride;
-            ca.R = R; ca.C = C; ca.pitch = g.pitch;
-            ca.n_strips = (C + kCasSW - 1) / kCasSW;
-            int E = 0;
-            for (int i = 5; i >= 1; --i) { E += py.krad[i]; ca.E[i - 1] = E; }
-            ca.E[5] = 0;
-            int dd = 0, T = 0;
-            for (int w = 0; w < 5; ++w) {
-                ca.K[w] = make_kern(py, w + 1);
-                ca.d[w] = dd;
-                ca.n[w] = (R + 2 * ca.E[w] + BS_P - 1) / BS_P * BS_P;   // inputs: rows -E_w .. R-1+E_w
-                T = std::max(T, dd + ca.n[w]);
-                dd += 2 * py.krad[w + 1] + 1;
-            }
-            ca.T = T;
-            if (o + 1 < o_small) {                                   // level L (wave 2) stores the next base
-                const OctGeom& ng = py.oct[o + 1];
-                ca.K[L - 1].nb = A + ng.g_off[0];
-                ca.K[L - 1].nb_pitch = ng.pitch; ca.K[L - 1].nb_rows = ng.rows; ca.K[L - 1].nb_cols = ng.cols;
-                base_done = true;
-            }
-            VO_LAUNCH_NAMED("k_oct0_cascade", k_oct0_cascade, dim3(ca.n_strips * n_img), dim3(320), 0, s, ca);
-            if (ev_o0) hipEventRecord(ev_o0, s);
-            continue;
-        }
 #if VO_EXPERIMENTAL
         if (o < n_fused) {
             octave_fused_launch(py, d_py, b, o, n_img, thr, s);
