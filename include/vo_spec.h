@@ -131,35 +131,26 @@ VO_HD float vo_rcp_nr(float d)
 VO_HD float vo_sift_wt(float s, int k) { return vo_expf_nonpos((float)(k * k) * s); }
 
 /* ------------------------------------------------------------------------ */
-/* atan2 in DEGREES, result in [0, 360).  (OpenCV fastAtan2 convention:      */
-/* angle of the vector (x, y), counter-clockwise from +x.)  Accurate to      */
-/* ~1e-5 deg; only basic ops.  Written select-only with ONE reciprocal so    */
-/* the SIMT form has no divergent branches: with lo = min(|x|,|y|), hi = max,*/
-/*   t = lo/hi            if lo <= tan(pi/8)*hi  (tested as a float product) */
-/*   t = (lo-hi)/(lo+hi)  otherwise, and atan(lo/hi) = pi/4 + atan(t),       */
-/* the quotient formed as num * vo_rcp_nr(den) (den clamped to >= 1e-30:    */
-/* |num| <= den, so |t| <= 1 everywhere and t = 0 at the origin).            */
+/* atan2 in DEGREES, result in [0, 360): OpenCV's fastAtan2 (the published  */
+/* 7th-order polynomial cv::hal::fastAtan2 applies in SIFT's orientation     */
+/* histogram and descriptor), with lo = min(|x|,|y|), hi = max:              */
+/*   c = lo / (hi + DBL_EPSILON),  a = (((p7 c^2 + p5) c^2 + p3) c^2 + p1) c */
+/* in degrees, then the octant/quadrant folds.  Deterministic form: the      */
+/* quotient is lo * vo_rcp_nr(hi + DBL_EPSILON) (within 2 ulp of OpenCV's    */
+/* division) and the Horner steps are fmaf; select-only, no branches.  The   */
+/* polynomial's own error against the true atan2 is < 0.01 deg.  A result    */
+/* that rounds up to 360 (y < 0 at a vanishing angle) wraps to 0.            */
 /* ------------------------------------------------------------------------ */
 VO_HD float vo_atan2_deg(float y, float x)
 {
     const float ax = fabsf(x), ay = fabsf(y);
     const int swap = ay > ax;
     const float lo = swap ? ax : ay, hi = swap ? ay : ax;
-    const int red = lo > 0.41421356f * hi;
-    const float num = red ? lo - hi : lo;
-    const float den = red ? lo + hi : hi;
-    const float t = num * vo_rcp_nr(den > 1e-30f ? den : 1e-30f);
-    const float t2 = t * t;
-    /* odd Taylor series to t^15, |t| <= tan(pi/8) -> truncation < 2e-8 */
-    float p = -1.0f / 15.0f;
-    p = fmaf(p, t2, 1.0f / 13.0f);
-    p = fmaf(p, t2, -1.0f / 11.0f);
-    p = fmaf(p, t2, 1.0f / 9.0f);
-    p = fmaf(p, t2, -1.0f / 7.0f);
-    p = fmaf(p, t2, 1.0f / 5.0f);
-    p = fmaf(p, t2, -1.0f / 3.0f);
-    p = p * t2;
-    float a = (fmaf(p, t, t) + (red ? 0.78539816339744831f : 0.0f)) * 57.295779513082321f;
+    const float c = lo * vo_rcp_nr(hi + 2.220446049250313e-16f);
+    const float c2 = c * c;
+    const float p1 = 0.9997878412794807f * 57.29577951308232f, p3 = -0.3258083974640975f * 57.29577951308232f;
+    const float p5 = 0.1555786518463281f * 57.29577951308232f, p7 = -0.04432655554792128f * 57.29577951308232f;
+    float a = fmaf(fmaf(fmaf(p7, c2, p5), c2, p3), c2, p1) * c;
     a = swap ? 90.0f - a : a;
     a = x < 0.0f ? 180.0f - a : a;
     a = y < 0.0f ? 360.0f - a : a;
@@ -304,9 +295,11 @@ VO_HD uint32_t vo_rand_index(uint32_t r, uint32_t n) { return (uint32_t)(((uint6
 /*    (hist_width <= 36.3): < 2.1e9 < 2^32;                                   */
 /*  - orientation: bins are summed in 64 bits (any window size).              */
 /* A bin converts back with one correct rounding: (float)sum * 2^-10.        */
+/* Rounding: floor(v + 1/2) (half up).  v + 1/2 is exact for v < 2^22, far  */
+/* above any weight, so this is one v_cvt_rpi_i32_f32 on the GPU.           */
 /* ------------------------------------------------------------------------ */
 #define VO_DESC_FX_SCALE 1024.0f
-VO_HD uint32_t vo_desc_fx_quant(float v_scaled) { return (uint32_t)rintf(v_scaled); }
+VO_HD uint32_t vo_desc_fx_quant(float v_scaled) { return (uint32_t)floorf(v_scaled + 0.5f); }
 VO_HD float vo_desc_fx_to_float(uint32_t s) { return (float)s * (1.0f / VO_DESC_FX_SCALE); }
 VO_HD float vo_hist_fx_to_float(uint64_t s) { return (float)s * (1.0f / VO_DESC_FX_SCALE); }
 

@@ -1451,6 +1451,16 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
     }
 }
 
+// One histogram weight to fixed point: vo_desc_fx_quant's floor(v + 1/2) is v_cvt_rpi_i32_f32
+// (exact: v + 1/2 is representable for every weight, v < 2^22; tests/test_gpu_golden.py and the
+// descriptor parity tests hold it to the oracle's floorf bit for bit)
+__device__ __forceinline__ uint32_t desc_fxq(float v)
+{
+    int r;
+    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(v));
+    return (uint32_t)r;
+}
+
 // Orientation assignment: one wave per accepted candidate (npk == -1).  Each
 // lane accumulates its samples' fixed-point weights (vo_desc_fx_quant, 2^-10)
 // into a private histogram hp[bin][lane]: lane l's words all lie in LDS bank l
@@ -1543,7 +1553,7 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
                 float ori = vo_atan2_deg(dy, dx);
                 int bin = vo_round((float)VO_SIFT_ORI_BINS / 360.0f * ori);   // ori in [0, 360): bin in [0, 36]
                 if (bin >= VO_SIFT_ORI_BINS) bin -= VO_SIFT_ORI_BINS;
-                const uint32_t qv = vo_desc_fx_quant((w * mag) * VO_DESC_FX_SCALE);
+                const uint32_t qv = desc_fxq((w * mag) * VO_DESC_FX_SCALE);
                 // private column, bank = lane; masked samples add 0; a returnless LDS add, so the
                 // update does not wait for the column's old value
                 atomicAdd(&hp[bin * NC + (lane & (NC - 1))], okk[q] ? qv : 0u);
@@ -1721,7 +1731,8 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
         sin_t = sin_t / hist_width;
         {
             const float wsc = exp_scale / (hist_width * hist_width);
-            for (int k2 = lane; k2 <= radius; k2 += 64) wtab[k2] = vo_sift_wt(wsc, k2);
+            // x 32 per factor: the product carries the fixed-point pre-scale 2^10 (exact, powers of two)
+            for (int k2 = lane; k2 <= radius; k2 += 64) wtab[k2] = vo_sift_wt(wsc, k2) * 32.0f;
         }
         // Only ~half of the (2r+1)^2 window lies inside the rotated 4x4-cell square.  Each
         // window row i gets a conservative column interval [jlo, jhi] (a superset: +-2
@@ -1798,7 +1809,7 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
             float rbin = r_rot + (float)(DW / 2) - 0.5f;
             float cbin = c_rot + (float)(DW / 2) - 0.5f;
             float ang = vo_atan2_deg(dy, dx);
-            float mag = (vo_grad_mag(dx, dy) * w) * VO_DESC_FX_SCALE;
+            float mag = vo_grad_mag(dx, dy) * w;         // = (|grad| w_ij) 2^10 exactly (w from the x 32 table)
             float obin = (ang - ori) * bins_per_deg;
             // floors kept in float ((float)(int)floorf(v) == floorf(v) here); the cell index is an
             // exact small-integer float expression, one conversion; obin in [-8, 8] so the circular
@@ -1806,7 +1817,9 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
             const float fr0 = floorf(rbin), fc0 = floorf(cbin), fo0 = floorf(obin);
             rbin -= fr0; cbin -= fc0; obin -= fo0;
             const int o0 = (int)fo0 & (DN - 1);
-            const int cell = (int)((fr0 + 1.0f) * (float)(DW + 2) + (fc0 + 1.0f));   // in [0, (DW+2)^2)
+            // histogram word of cell (fr0 + 1, fc0 + 1): ((fr0 + 1) (DW + 2) + fc0 + 1) DBS as two
+            // exact small-integer fmas (< 2^24), one conversion
+            const float cell_w = fmaf(fr0, (float)((DW + 2) * DBS), fmaf(fc0, (float)DBS, (float)((DW + 3) * DBS)));
             float v_r1 = mag * rbin, v_r0 = mag - v_r1;
             float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
             float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
@@ -1814,15 +1827,15 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
             float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
             float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
             float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-            uint32_t* h = hc + (int)((float)cell * (float)DBS) + o0;     // exact: < 2^24
-            atomicAdd(h, vo_desc_fx_quant(v_rco000));
-            atomicAdd(h + 1, vo_desc_fx_quant(v_rco001));
-            atomicAdd(h + DBS, vo_desc_fx_quant(v_rco010));
-            atomicAdd(h + DBS + 1, vo_desc_fx_quant(v_rco011));
-            atomicAdd(h + (DW + 2) * DBS, vo_desc_fx_quant(v_rco100));
-            atomicAdd(h + (DW + 2) * DBS + 1, vo_desc_fx_quant(v_rco101));
-            atomicAdd(h + (DW + 3) * DBS, vo_desc_fx_quant(v_rco110));
-            atomicAdd(h + (DW + 3) * DBS + 1, vo_desc_fx_quant(v_rco111));
+            uint32_t* h = hc + (int)cell_w + o0;
+            atomicAdd(h, desc_fxq(v_rco000));
+            atomicAdd(h + 1, desc_fxq(v_rco001));
+            atomicAdd(h + DBS, desc_fxq(v_rco010));
+            atomicAdd(h + DBS + 1, desc_fxq(v_rco011));
+            atomicAdd(h + (DW + 2) * DBS, desc_fxq(v_rco100));
+            atomicAdd(h + (DW + 2) * DBS + 1, desc_fxq(v_rco101));
+            atomicAdd(h + (DW + 3) * DBS, desc_fxq(v_rco110));
+            atomicAdd(h + (DW + 3) * DBS + 1, desc_fxq(v_rco111));
         };
         // the gradient neighbours of a listed sample (every listed sample is interior): x+1, x-1 as
         // one 12-B load (through a 3-float type declared with the 4-B alignment the address has),
