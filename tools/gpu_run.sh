@@ -1,7 +1,7 @@
 #!/bin/bash
 # One evidence pass on a GPU box (run through gpurun from the repo root):
 #   bash tools/gpu_run.sh <outdir> [steps...]
-# steps (default: tests smoke bench): tests | smoke | bench | distbench | kprof | seqprof | pmc | attr | batch:<B> | probe:<tools binary>
+# steps (default: tests smoke bench): tests | smoke | bench | distbench | kprof | seqprof | pmc | insitu | attr | batch:<B> | probe:<tools binary>
 #   | gpuonly:<pytest -k expr, + for spaces> | vtests:<variant>:<expr> | ab:<variant>[,<variant>...] (tools/variants/<name>/libvo.so)
 # Every GPU step has its own time limit and the chain stops at the first failure.
 set -e
@@ -51,6 +51,13 @@ for st in $STEPS; do
   pmc)
     timeout -k 10 900 bash tools/pmc_passes.sh _$(basename $O) > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
     echo pmc-done ;;
+  insitu)
+    # kernel trace of the asynchronous loop + the counter passes -> tools/insitu_model.py
+    timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $O/itrace -o t -- python3 tools/prof_run.py 64 6 > $O/itrace.log 2>&1 \
+      || { tail -20 $O/itrace.log; exit 1; }
+    timeout -k 10 900 bash tools/pmc_passes.sh _$(basename $O) > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
+    python3 tools/insitu_model.py gpurun_out/pmc_$(basename $O) $(find $O/itrace -name "*kernel_trace.csv" | head -1) $O/insitu.json
+    python3 tools/pmc_traffic.py gpurun_out/pmc_$(basename $O) $O/pmc_traffic.json > /dev/null ;;
   batch:*)
     b=${st#batch:}
     for bb in 64 $b 64; do
