@@ -1327,6 +1327,63 @@ __device__ __forceinline__ void flat_find(const int* pre, int n_img, long t, int
     k = (int)(t - pre[lo]);
 }
 
+// flat_find for one whole wave (all 64 lanes active, t wave-uniform): the prefix is nondecreasing,
+// so the image is the number of i in [1, n_img) with pre[i] <= t -- one round of independent LDS
+// reads and ballots instead of a binary search's chain of dependent reads
+__device__ __forceinline__ void flat_find_wave(const int* pre, int n_img, long t, int& img, int& k)
+{
+    const int lane = threadIdx.x & 63;
+    int cnt = 0;
+#pragma unroll
+    for (int b = 0; b < VO_FLAT_MAX_IMG; b += 64) {
+        if (b >= n_img - 1) break;                      // uniform
+        const int i = b + 1 + lane;
+        cnt += __popcll(__ballot(i < n_img && pre[i] <= t));
+    }
+    img = cnt;
+    k = (int)(t - pre[cnt]);
+}
+
+// Cross-lane trees without LDS (gfx950 v_permlane32_swap / v_permlane16_swap and DPP row shifts).
+// wave_tree_sum: lane 0's value is the pairwise tree of the shfl_down(32, 16, .., 1) loop, bit for
+// bit (each step adds lane l + st to lane l), returned to every lane.
+template <typename T>
+__device__ __forceinline__ T wave_tree_sum(T v)
+{
+    auto bits = [](T x) { return __builtin_bit_cast(int, x); };
+    auto val = [](int x) { return __builtin_bit_cast(T, x); };
+    v = v + val(__builtin_amdgcn_permlane32_swap(bits(v), bits(v), false, false)[1]);   // lanes < 32: v[l + 32]
+    v = v + val(__builtin_amdgcn_permlane16_swap(bits(v), bits(v), false, false)[1]);   // lanes < 16: v[l + 16]
+    v = v + val(__builtin_amdgcn_update_dpp(0, bits(v), 0x108, 0xF, 0xF, true));        // row_shl:8
+    v = v + val(__builtin_amdgcn_update_dpp(0, bits(v), 0x104, 0xF, 0xF, true));        // row_shl:4
+    v = v + val(__builtin_amdgcn_update_dpp(0, bits(v), 0x102, 0xF, 0xF, true));        // row_shl:2
+    v = v + val(__builtin_amdgcn_update_dpp(0, bits(v), 0x101, 0xF, 0xF, true));        // row_shl:1
+    return val(__builtin_amdgcn_readlane(bits(v), 0));
+}
+// maximum over the 64 lanes (order-free), returned to every lane
+__device__ __forceinline__ float wave_max(float v)
+{
+    auto bits = [](float x) { return __float_as_int(x); };
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_permlane32_swap(bits(v), bits(v), false, false)[1]));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_permlane16_swap(bits(v), bits(v), false, false)[1]));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(bits(v), bits(v), 0x108, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(bits(v), bits(v), 0x104, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(bits(v), bits(v), 0x102, 0xF, 0xF, false)));
+    v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(bits(v), bits(v), 0x101, 0xF, 0xF, false)));
+    return __int_as_float(__builtin_amdgcn_readlane(bits(v), 0));
+}
+// inclusive prefix sum over the 64 lanes (integers): row shifts, then the row broadcasts
+__device__ __forceinline__ int wave_incl_scan(int x)
+{
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 into rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 into rows 2, 3
+    return x;
+}
+
 // sqrtf(x), correctly rounded, for x == +0 or 2^-96 <= x < inf: the compiler's IEEE sqrt less its
 // small-argument scaling and special-class select -- v_sqrt_f32 and the same two one-ulp
 // residual corrections, so the value is sqrtf's.  The gradient magnitudes call it on sums of
@@ -1496,7 +1553,7 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
     const long total = flat_setup(n_cand, cand_cap, n_img, fpre);
     for (long t = blockIdx.x; t < total; t += gridDim.x) {
         int img, kidx;
-        flat_find(fpre, n_img, t, img, kidx);
+        flat_find_wave(fpre, n_img, t, img, kidx);
         CandOut* out = cout + (size_t)img * cand_cap + kidx;
         if (__builtin_amdgcn_readfirstlane(out->npk) != -1) continue;
         const int o = __builtin_amdgcn_readfirstlane(out->o), layer = __builtin_amdgcn_readfirstlane(out->layer);
@@ -1573,9 +1630,7 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
             hv = (m2 + p2) * (1.0f / 16.0f) + (m1 + p1) * (4.0f / 16.0f) + tf[lane] * (6.0f / 16.0f);
             hs[lane] = hv;
         }
-        float mx = hv;
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+        const float mx = wave_max(hv);
         __syncthreads();
         const float mag_thr = mx * VO_SIFT_ORI_PEAK;
         bool pk = false;
@@ -1706,7 +1761,7 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
     const long total = flat_setup(n_kp, kp_cap, n_img, fpre);
     for (long t = blockIdx.x; t < total; t += gridDim.x) {
         int img, k;
-        flat_find(fpre, n_img, t, img, k);
+        flat_find_wave(fpre, n_img, t, img, k);
         KpInt q = kpi[(size_t)img * kp_cap + k];
         q.o = __builtin_amdgcn_readfirstlane(q.o);              // wave-uniform -> scalar geometry loads
         q.layer = __builtin_amdgcn_readfirstlane(q.layer);
@@ -1791,9 +1846,7 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
                 ent[q] = (q < per && r0w + q < nrows) ? rtab[r0w + q] : 0u;
                 sum += (int)(ent[q] & 0xFFFFu);
             }
-            int inc = sum;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(inc, o); if (lane >= o) inc += y; }
+            const int inc = wave_incl_scan(sum);
             int acc = inc - sum;
 #pragma unroll
             for (int q = 0; q < PER_MAX; ++q)
@@ -1937,17 +1990,11 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
             }
             dv[h] = vo_desc_fx_to_float(v);
         }
-        float s = dv[0] * dv[0] + dv[1] * dv[1];
-#pragma unroll
-        for (int st = 32; st >= 1; st >>= 1) s = s + __shfl_down(s, st);
-        const float nrm0 = __shfl(s, 0);
+        const float nrm0 = wave_tree_sum(dv[0] * dv[0] + dv[1] * dv[1]);
         const float thr = sqrtf(nrm0) * VO_SIFT_DESCR_MAG_THR;
         dv[0] = dv[0] < thr ? dv[0] : thr;
         dv[1] = dv[1] < thr ? dv[1] : thr;
-        s = dv[0] * dv[0] + dv[1] * dv[1];
-#pragma unroll
-        for (int st = 32; st >= 1; st >>= 1) s = s + __shfl_down(s, st);
-        const float nrm = sqrtf(__shfl(s, 0));
+        const float nrm = sqrtf(wave_tree_sum(dv[0] * dv[0] + dv[1] * dv[1]));
         const float scale = VO_SIFT_DESCR_INT_FCTR / (nrm > VO_FLT_EPSILON ? nrm : VO_FLT_EPSILON);
         int qv[2];
 #pragma unroll
@@ -1958,9 +2005,7 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
         uint8_t* dst = desc + ((size_t)img * kp_cap + k) * VO_DESC_LEN;
         dst[lane] = (uint8_t)qv[0];
         dst[lane + 64] = (uint8_t)qv[1];
-        int sum = qv[0] + qv[1], sq = qv[0] * qv[0] + qv[1] * qv[1];
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) { sum += __shfl_xor(sum, off); sq += __shfl_xor(sq, off); }
+        const int sum = wave_tree_sum(qv[0] + qv[1]), sq = wave_tree_sum(qv[0] * qv[0] + qv[1] * qv[1]);
         if (lane == 0) {
             DescMeta m;
             m.sum = sum;
