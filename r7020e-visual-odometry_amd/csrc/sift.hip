@@ -1291,59 +1291,6 @@ __global__ __launch_bounds__(256) void k_seg_emit(const Pyramid* __restrict__ py
 // pre[i] <= t < pre[i+1], pre[i+1] = pre[i] + min(counts[i], cap).  The prefix
 // is built once per block in LDS (all threads call flat_setup); flat_find is
 // then a binary search instead of a per-item walk over the images.
-#define VO_FLAT_MAX_IMG 258     // 2 * max_batch(128) + 2 image slots
-__device__ __forceinline__ long flat_setup(const int* __restrict__ counts, int cap, int n_img, int* pre)
-{
-    const int tid = threadIdx.x, nt = blockDim.x;
-    __shared__ int carry;
-    if (tid == 0) { carry = 0; pre[0] = 0; }
-    __syncthreads();
-    for (int b0 = 0; b0 < n_img; b0 += 64) {          // the first wave scans 64 images per round
-        if (tid < 64) {
-            const int i = b0 + tid;
-            int c = i < n_img ? min(counts[i], cap) : 0;
-            int x = c;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) { const int y = __shfl_up(x, o); if (tid >= o) x += y; }
-            const int base = carry;
-            if (i < n_img) pre[i + 1] = base + x;
-            const int tot = __shfl(x, 63);
-            if (tid == 0) carry = base + tot;
-        }
-        __syncthreads();
-    }
-    (void)nt;
-    return pre[n_img];
-}
-
-__device__ __forceinline__ void flat_find(const int* pre, int n_img, long t, int& img, int& k)
-{
-    int lo = 0, hi = n_img - 1;                       // largest i with pre[i] <= t
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (pre[mid] <= t) lo = mid; else hi = mid - 1;
-    }
-    img = lo;
-    k = (int)(t - pre[lo]);
-}
-
-// flat_find for one whole wave (all 64 lanes active, t wave-uniform): the prefix is nondecreasing,
-// so the image is the number of i in [1, n_img) with pre[i] <= t -- one round of independent LDS
-// reads and ballots instead of a binary search's chain of dependent reads
-__device__ __forceinline__ void flat_find_wave(const int* pre, int n_img, long t, int& img, int& k)
-{
-    const int lane = threadIdx.x & 63;
-    int cnt = 0;
-#pragma unroll
-    for (int b = 0; b < VO_FLAT_MAX_IMG; b += 64) {
-        if (b >= n_img - 1) break;                      // uniform
-        const int i = b + 1 + lane;
-        cnt += __popcll(__ballot(i < n_img && pre[i] <= t));
-    }
-    img = cnt;
-    k = (int)(t - pre[cnt]);
-}
-
 // Cross-lane trees without LDS (gfx950 v_permlane32_swap / v_permlane16_swap and DPP row shifts).
 // wave_tree_sum: lane 0's value is the pairwise tree of the shfl_down(32, 16, .., 1) loop, bit for
 // bit (each step adds lane l + st to lane l), returned to every lane.
@@ -1382,6 +1329,57 @@ __device__ __forceinline__ int wave_incl_scan(int x)
     x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 into rows 1, 3
     x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 into rows 2, 3
     return x;
+}
+
+#define VO_FLAT_MAX_IMG 258     // 2 * max_batch(128) + 2 image slots
+__device__ __forceinline__ long flat_setup(const int* __restrict__ counts, int cap, int n_img, int* pre)
+{
+    const int tid = threadIdx.x, nt = blockDim.x;
+    __shared__ int carry;
+    if (tid == 0) { carry = 0; pre[0] = 0; }
+    __syncthreads();
+    for (int b0 = 0; b0 < n_img; b0 += 64) {          // the first wave scans 64 images per round
+        if (tid < 64) {
+            const int i = b0 + tid;
+            const int c = i < n_img ? min(counts[i], cap) : 0;
+            const int x = wave_incl_scan(c);               // (wave 0 whole: tid < 64)
+            const int base = carry;
+            if (i < n_img) pre[i + 1] = base + x;
+            const int tot = __builtin_amdgcn_readlane(x, 63);
+            if (tid == 0) carry = base + tot;
+        }
+        __syncthreads();
+    }
+    (void)nt;
+    return pre[n_img];
+}
+
+__device__ __forceinline__ void flat_find(const int* pre, int n_img, long t, int& img, int& k)
+{
+    int lo = 0, hi = n_img - 1;                       // largest i with pre[i] <= t
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    img = lo;
+    k = (int)(t - pre[lo]);
+}
+
+// flat_find for one whole wave (all 64 lanes active, t wave-uniform): the prefix is nondecreasing,
+// so the image is the number of i in [1, n_img) with pre[i] <= t -- one round of independent LDS
+// reads and ballots instead of a binary search's chain of dependent reads
+__device__ __forceinline__ void flat_find_wave(const int* pre, int n_img, long t, int& img, int& k)
+{
+    const int lane = threadIdx.x & 63;
+    int cnt = 0;
+#pragma unroll
+    for (int b = 0; b < VO_FLAT_MAX_IMG; b += 64) {
+        if (b >= n_img - 1) break;                      // uniform
+        const int i = b + 1 + lane;
+        cnt += __popcll(__ballot(i < n_img && pre[i] <= t));
+    }
+    img = cnt;
+    k = (int)(t - pre[cnt]);
 }
 
 // sqrtf(x), correctly rounded, for x == +0 or 2^-96 <= x < inf: the compiler's IEEE sqrt less its
