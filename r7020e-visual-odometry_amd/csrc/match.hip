@@ -8,8 +8,8 @@
 //   dot(a,b) = dot(a',b') + 128 (sum a + sum b) - 2^21,
 // so the result is exact and order-free; MFMA throughput is 8x the v_dot4
 // VALU path.  The top-2 search is fused into the MFMA epilogue: each lane keeps
-// (best, idx, second) for its 16 accumulator rows, halves merge by xor
-// shuffles with a (value, index) total order, chunks of F2 merge in
+// (best, idx, second) for its 16 accumulator rows, halves merge by DPP rotations
+// and a permlane swap with a (value, index) total order, chunks of F2 merge in
 // k_match_merge (one thread per F1 row), which also applies MatchThreshold /
 // MaxRatio; k_match_compact writes the pairs in ascending F1 order with a block
 // prefix sum.
@@ -36,6 +36,52 @@ __device__ __forceinline__ void top2c_merge(float& b, int& i, float& s, float b2
     const float ns = fmaxf(fmaxf(s, s2), fminf(b, b2));
     if (b2 > b || (b2 == b && i2 < i)) { b = b2; i = i2; }
     s = ns;
+}
+
+// Cross-lane steps within a 32-lane half without LDS: DPP row rotations (every lane of a
+// 16-lane row receives a valid source) and v_permlane16_swap for the other row of the half.
+// The merges they feed (max, top2c_merge) are associative and commutative, so rotations
+// give every lane the same result as the xor butterfly.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v)
+{
+    return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v)
+{
+    return __int_as_float(dpp_i<CTRL>(__float_as_int(v)));
+}
+__device__ __forceinline__ int xor16_i(int v)               // the value of lane l ^ 16
+{
+    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (threadIdx.x & 16) ? p[0] : p[1];
+}
+__device__ __forceinline__ float xor16_f(float v)
+{
+    return __int_as_float(xor16_i(__float_as_int(v)));
+}
+enum : int { VO_DPP_ROR1 = 0x121, VO_DPP_ROR2 = 0x122, VO_DPP_ROR4 = 0x124, VO_DPP_ROR8 = 0x128 };
+__device__ __forceinline__ float half_max(float m)           // max over the lane's 32-lane half
+{
+    m = fmaxf(m, dpp_f<VO_DPP_ROR8>(m));
+    m = fmaxf(m, dpp_f<VO_DPP_ROR4>(m));
+    m = fmaxf(m, dpp_f<VO_DPP_ROR2>(m));
+    m = fmaxf(m, dpp_f<VO_DPP_ROR1>(m));
+    return fmaxf(m, xor16_f(m));
+}
+template <int CTRL>
+__device__ __forceinline__ void top2c_step(float& b, int& i, float& s)
+{
+    top2c_merge(b, i, s, dpp_f<CTRL>(b), dpp_i<CTRL>(i), dpp_f<CTRL>(s));
+}
+__device__ __forceinline__ void half_top2c(float& b, int& i, float& s)   // merge over the 32-lane half
+{
+    top2c_step<VO_DPP_ROR8>(b, i, s);
+    top2c_step<VO_DPP_ROR4>(b, i, s);
+    top2c_step<VO_DPP_ROR2>(b, i, s);
+    top2c_step<VO_DPP_ROR1>(b, i, s);
+    top2c_merge(b, i, s, xor16_f(b), xor16_i(i), xor16_f(s));
 }
 
 // Pointers read from the job table are generic to the compiler, so loads through them became
@@ -84,7 +130,8 @@ __device__ __forceinline__ v4i load_frag(const uint8_t* row, int off)
 // is written to LDS and tile t+2 is in flight from HBM/L2 while tile t runs its 4 MFMAs
 // and epilogue.  Epilogue per accumulator element: dot = acc + 128 sa - 2^21 + 128 sb (one
 // add3), c = ((float)dot * inv|a|) * inv|b| (packed muls, two rows at once), then the top-2
-// update, skipped by the wave when no lane's c beats its row's second best.
+// update, skipped by the wave when no lane's c beats its row's second best.  The half-wave
+// reductions (second-best refresh, final merge) use DPP rotations and v_permlane16_swap.
 #define MP_ROWS 128
 #define MP_LDS_ROW 144
 #define VO_MP_MAX_JOBS 256        // jobs per launch (one per thread of the task-table prologue)
@@ -234,25 +281,12 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
             ++tno;
             if ((tno & (tno - 1)) == 0) {                  // wave-uniform
 #pragma unroll
-                for (int reg = 0; reg < 16; ++reg) {
-                    float m = second[reg];
-#pragma unroll
-                    for (int off = 16; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-                    second[reg] = m;
-                }
+                for (int reg = 0; reg < 16; ++reg) second[reg] = half_max(second[reg]);
             }
         }
         // merge the 32 lanes of each half (same accumulator rows, different columns)
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-#pragma unroll
-            for (int off = 16; off >= 1; off >>= 1) {
-                const float b2 = __shfl_xor(best[reg], off);
-                const int i2 = __shfl_xor(bidx[reg], off);
-                const float s2 = __shfl_xor(second[reg], off);
-                top2c_merge(best[reg], bidx[reg], second[reg], b2, i2, s2);
-            }
-        }
+        for (int reg = 0; reg < 16; ++reg) half_top2c(best[reg], bidx[reg], second[reg]);
         if (l31 < 16) {
             // lane l31 of half h writes accumulator row `l31` (select by unrolled compare)
             float bb = -INFINITY, ss = -INFINITY;

@@ -428,7 +428,10 @@ __device__ __forceinline__ void vo_dpp_window(const vec_t& vm, float* w)
 // the P steps of 16-B stores issued before it -- the base kernel's stream of 1 GB of stores was
 // paced by its tiny u8 loads.  With the loads gone the loop never waits on vmcnt.
 struct U8Src { const uint8_t* p; int ld, rows, cols; };
-constexpr int kBaseMaxTH = 128;                               // band height bound of the staged form
+#ifndef VO_BASE_MAX_TH
+#define VO_BASE_MAX_TH 128
+#endif
+constexpr int kBaseMaxTH = VO_BASE_MAX_TH;                    // band height bound of the staged form
 // staged row length in dwords: the upsampled span of a wave (64 CPL columns + 2 RH halo) needs
 // (64 CPL + 2 RH) / 2 + 3 source bytes; + 3 for the row's misalignment, + 4 for the word pair
 __host__ __device__ constexpr int bs_u8_dw(int r, int cpl) { return ((64 * cpl + 2 * bs_rh(r, cpl)) / 2 + 3 + 3 + 4 + 3) / 4; }
@@ -2067,8 +2070,8 @@ static bool launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
         const int cpl = (!base && C <= kCpl2MaxC) ? 2 : 4;
         const int n_strips = (C + 64 * cpl - 1) / (64 * cpl);
         const long rows_total = (long)R * n_strips * grid.z;
-        static_assert(kMaxTH <= kBaseMaxTH, "the staged octave-0 base stages at most kBaseMaxTH-row bands");
-        int TH = (int)std::min<long>(kMaxTH, rows_total / kWaveTarget);
+        // (the staged octave-0 base stages at most kBaseMaxTH-row bands: its LDS is sized for them)
+        int TH = (int)std::min<long>(base ? std::min(kMaxTH, kBaseMaxTH) : kMaxTH, rows_total / kWaveTarget);
         TH = std::max(BS_P, TH / BS_P * BS_P);
         if (R >= TH && R > RAD + BS_P + 2) {             // (one reflection fold per band edge)
             const int n_bands = (R + TH - 1) / TH;
