@@ -429,7 +429,7 @@ __device__ __forceinline__ void vo_dpp_window(const vec_t& vm, float* w)
 // paced by its tiny u8 loads.  With the loads gone the loop never waits on vmcnt.
 struct U8Src { const uint8_t* p; int ld, rows, cols; };
 #ifndef VO_BASE_MAX_TH
-#define VO_BASE_MAX_TH 128
+#define VO_BASE_MAX_TH 96         // 8.7 KB of staged rows: 16 one-wave workgroups per CU fit (128: 11.1 KB, 14)
 #endif
 constexpr int kBaseMaxTH = VO_BASE_MAX_TH;                    // band height bound of the staged form
 // staged row length in dwords: the upsampled span of a wave (64 CPL columns + 2 RH halo) needs
@@ -793,8 +793,11 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
 #ifndef VO_BLUR_OCC3_MAXR
 #define VO_BLUR_OCC3_MAXR 6       // radii up to this run at 3 waves per SIMD (168 VGPRs), larger at 2
 #endif
+#ifndef VO_BASE_WAVES
+#define VO_BASE_WAVES 3           // register budget of the staged octave-0 base (TAG & 4), waves per SIMD
+#endif
 template <int RAD, int TAG, int CPL = 4>
-__global__ __launch_bounds__(64, (RAD <= VO_BLUR_OCC3_MAXR || CPL == 2) ? 3 : 2) void k_blur_stream(
+__global__ __launch_bounds__(64, (TAG & 4) ? VO_BASE_WAVES : (RAD <= VO_BLUR_OCC3_MAXR || CPL == 2) ? 3 : 2) void k_blur_stream(
     const float* __restrict__ src, size_t splane, size_t dplane, int pitch, int R, int C, float* __restrict__ g_out, Kern K,
     int n_strips, int n_bands, int TH, ImageSrc isrc, int in_rows, int in_cols)
 {
