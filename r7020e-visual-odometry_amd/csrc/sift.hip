@@ -1553,7 +1553,7 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
     __shared__ float tf[VO_SIFT_ORI_BINS];
     __shared__ float hs[VO_SIFT_ORI_BINS];
     const int lane = threadIdx.x;
-    __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
+    extern __shared__ int fpre[];                    // n_img + 1 ints (dynamic: sized by the launch)
     const long total = flat_setup(n_cand, cand_cap, n_img, fpre);
     for (long t = blockIdx.x; t < total; t += gridDim.x) {
         int img, kidx;
@@ -1746,7 +1746,8 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
 template <int DCOPIES>
 __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                              const KpInt* __restrict__ kpi, const int* __restrict__ n_kp,
-                                             uint8_t* __restrict__ desc, DescMeta* __restrict__ meta, int kp_cap, int n_img)
+                                             uint8_t* __restrict__ desc, DescMeta* __restrict__ meta, int kp_cap, int n_img,
+                                             int rcap)
 {
     static_assert(DCS >= DHIST, "copy stride holds a histogram");
     __shared__ __attribute__((aligned(16))) uint32_t hfx[DCOPIES * DCS];
@@ -1755,13 +1756,20 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
     // start.  Starts fit 16 bits: a window never holds more than its (2 r + 1)^2 square, which
     // the cap r <= VO_SIFT_DESCR_RMAX = 127 bounds by 65025 (the rotated square alone is
     // ~2 r^2 + O(r) samples, but a capped radius can leave the whole square inside it).
-    // 7.8 KB of LDS with the histograms and weights -> 5 one-wave workgroups per SIMD.
+    // 6.3 KB of LDS with the histograms, tables and prefix at batch 64 -> 5 one-wave workgroups
+    // per SIMD with room to spare for the blur waves beside them.
     static_assert((2 * VO_SIFT_DESCR_RMAX + 1) * (2 * VO_SIFT_DESCR_RMAX + 1) <= 0xFFFF, "16-bit row starts");
-    __shared__ uint32_t rtab[2 * VO_SIFT_DESCR_RMAX + 2 + 8];
-    // separable window weights (vo_spec.h vo_sift_wt): w(i, j) = wtab[|i|] * wtab[|j|]; 0.5 KB
-    __shared__ float wtab[VO_SIFT_DESCR_RMAX + 1];
+    // Dynamic LDS, sized by the launch for this pyramid (desc_lds_bytes): the row table (2 rcap + 10
+    // entries), the separable window weights wtab[0 .. rcap] (vo_spec.h vo_sift_wt: w(i, j) =
+    // wtab[|i|] * wtab[|j|]) and the image prefix (n_img + 1).  rcap bounds every keypoint's radius
+    // (the largest refined scale the parameters allow, capped at VO_SIFT_DESCR_RMAX): 1.1 KB instead
+    // of 2.6 KB at the default parameters, so the descriptor's one-wave workgroups leave LDS for the
+    // scale-space waves that share their CUs.
+    extern __shared__ uint32_t dyn[];
+    uint32_t* const rtab = dyn;
+    float* const wtab = reinterpret_cast<float*>(dyn + 2 * rcap + 10);
+    int* const fpre = reinterpret_cast<int*>(dyn + 3 * rcap + 11);
     const int lane = threadIdx.x;
-    __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
     const long total = flat_setup(n_kp, kp_cap, n_img, fpre);
     for (long t = blockIdx.x; t < total; t += gridDim.x) {
         int img, k;
@@ -1786,6 +1794,7 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
         int radius = vo_round(hist_width * 1.4142135623730951f * (float)(DW + 1) * 0.5f);
         if (radius > g.dmax) radius = g.dmax;
         if (radius > VO_SIFT_DESCR_RMAX) radius = VO_SIFT_DESCR_RMAX;
+        radius = min(radius, rcap);                 // (never binds: rcap bounds every refined scale)
         cos_t = cos_t / hist_width;
         sin_t = sin_t / hist_width;
         {
@@ -2286,6 +2295,16 @@ void sift_enqueue_pyramid_tail(const Pyramid& py, SiftBuffers& b, int n_img, con
     sift_enqueue_extrema(py, b, n_img, p, s, d_py, ext_o_begin, py.n_oct);
 }
 
+// Largest descriptor window radius any keypoint can have: k_refine accepts layer <= L with
+// |xi| < 0.5, so the octave-relative scale stays below sigma 2^((L + 0.5) / L); the radius formula
+// of k_desc on that bound, + 2 for float rounding, capped at VO_SIFT_DESCR_RMAX (sizes k_desc's LDS).
+static int desc_radius_cap(const Pyramid& py, const vo_sift_params& p)
+{
+    const double scl = p.sigma * std::exp2((py.L + 0.5) / py.L);
+    const double r = VO_SIFT_DESCR_SCL * scl * 1.4142135623730951 * (VO_SIFT_DESCR_W + 1) * 0.5;
+    return (int)std::min<double>(VO_SIFT_DESCR_RMAX, std::ceil(r) + 2);
+}
+
 void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
                            const Pyramid* d_py)
 {
@@ -2296,14 +2315,17 @@ void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const v
     VO_LAUNCH(k_seg_emit, gs, dim3(256), 0, s, d_py, b.mask, (const uint32_t*)b.woff, b.cand, b.cand_cap);
     VO_LAUNCH(k_refine, dim3(512), dim3(256), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.cand_cap, n_img,
               p.contrast_threshold, p.edge_threshold, p.sigma);
-    VO_LAUNCH_NAMED("k_orient", (k_orient<36>), dim3(kFeatureGrid), dim3(64), 0, s, d_py, A, b.n_cand,
+    const size_t fpre_bytes = sizeof(int) * (size_t)(n_img + 1);
+    VO_LAUNCH_NAMED("k_orient", (k_orient<36>), dim3(kFeatureGrid), dim3(64), fpre_bytes, s, d_py, A, b.n_cand,
                     b.cout, b.cand_cap, n_img);
     VO_LAUNCH(k_scan_cands, dim3(n_img), dim3(1024), 0, s, b.cout, b.n_cand, b.koff, b.n_kp, b.cand_cap);
     VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, b.n_cand, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
                        n_img, p.upsample);
     // 4 histogram copies: 2 -> +4 %, 8 -> +33 % k_desc time (MI355X)
-    VO_LAUNCH_NAMED("k_desc", (k_desc<VO_DESC_COPIES>), dim3(kFeatureGrid), dim3(64), 0, s, d_py, A, b.kpi, b.n_kp, b.desc,
-                    b.meta, b.kp_cap, n_img);
+    const int rcap = desc_radius_cap(py, p);
+    VO_LAUNCH_NAMED("k_desc", (k_desc<VO_DESC_COPIES>), dim3(kFeatureGrid), dim3(64),
+                    sizeof(uint32_t) * (size_t)(3 * rcap + 11) + fpre_bytes, s, d_py, A, b.kpi, b.n_kp, b.desc,
+                    b.meta, b.kp_cap, n_img, rcap);
 }
 
 void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img, const vo_sift_params& p,
