@@ -1533,10 +1533,12 @@ __device__ __forceinline__ uint32_t desc_fxq(float v)
 // iteration with every gradient load issued first.  Smoothing, peak test and
 // interpolation as the oracle.  (A lane's u32 partial of one bin holds < 11k
 // samples' weights: windows up to ~7e5 samples.)
-// 32 histogram columns (lanes l and l+32 share one through returnless LDS adds): 5.9 KB of LDS
-// instead of 10.5 KB, so 5 waves per SIMD instead of 3.75 (k_orient 0.68 -> 0.53 ms isolated)
+// 16 histogram columns (lanes l, l+16, l+32, l+48 share one through returnless LDS adds): 2.3 KB
+// of histogram instead of 10.5 KB at 64 columns -- 32 columns took k_orient 0.68 -> 0.53 ms (5
+// waves per SIMD instead of 3.75), 16 columns 0.46-0.48 -> 0.44 ms isolated and 0.63-0.66 -> 0.57
+// in situ, where the LDS it leaves goes to the blur waves sharing its CUs (profiles/r04_zc_*)
 #ifndef VO_ORIENT_COLS
-#define VO_ORIENT_COLS 32
+#define VO_ORIENT_COLS 16
 #endif
 #ifndef VO_ORIENT_WAVES
 #define VO_ORIENT_WAVES 1
@@ -1548,7 +1550,7 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
 {
     // HS: bins per lane column (>= 36).  Layout hp[bin * 64 + lane].
     constexpr int NC = VO_ORIENT_COLS;             // histogram columns: lane l adds into column l % NC
-    static_assert(HS >= VO_SIFT_ORI_BINS && (HS * NC) % 4 == 0 && (NC == 64 || NC == 32), "columns hold the 36 bins");
+    static_assert(HS >= VO_SIFT_ORI_BINS && (HS * NC) % 4 == 0 && (NC == 64 || NC == 32 || NC == 16), "columns hold the 36 bins");
     __shared__ __attribute__((aligned(16))) uint32_t hp[HS * NC];
     __shared__ float tf[VO_SIFT_ORI_BINS];
     __shared__ float hs[VO_SIFT_ORI_BINS];
