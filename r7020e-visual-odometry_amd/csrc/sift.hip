@@ -1524,15 +1524,13 @@ __device__ __forceinline__ uint32_t desc_fxq(float v)
 
 // Orientation assignment: one wave per accepted candidate (npk == -1).  Each
 // lane accumulates its samples' fixed-point weights (vo_desc_fx_quant, 2^-10)
-// into a private histogram hp[bin][lane]: lane l's words all lie in LDS bank l
-// (64 banks x 4 B), so the scattered per-sample adds of a wave never collide on
-// a bank (zeroed with 16-B stores); the 36 bins are then summed over the 64
-// lanes in 64 bits (integer sums: identical to the oracle's sequential total),
-// lane b reading bin b's partials in a rotated order so the 36 reading lanes
-// are on 36 distinct banks at every step.  Samples are processed 4 per lane per
-// iteration with every gradient load issued first.  Smoothing, peak test and
-// interpolation as the oracle.  (A lane's u32 partial of one bin holds < 11k
-// samples' weights: windows up to ~7e5 samples.)
+// into histogram column l mod NC, hp[bin][column] (column c's words lie in LDS
+// banks c mod 64; zeroed with 16-B stores); the 36 bins are then summed over the
+// NC columns in 64 bits (integer sums: identical to the oracle's sequential
+// total), lane b reading bin b's partials in a rotated order.  Samples are
+// processed 4 per lane per iteration with every gradient load issued first.
+// Smoothing, peak test and interpolation as the oracle.  (A column's u32 partial
+// of one bin holds < 11k samples' weights: windows up to NC x 11k samples.)
 // 16 histogram columns (lanes l, l+16, l+32, l+48 share one through returnless LDS adds): 2.3 KB
 // of histogram instead of 10.5 KB at 64 columns -- 32 columns took k_orient 0.68 -> 0.53 ms (5
 // waves per SIMD instead of 3.75), 16 columns 0.46-0.48 -> 0.44 ms isolated and 0.63-0.66 -> 0.57
@@ -1624,7 +1622,7 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
         }
         __syncthreads();
         if (lane < VO_SIFT_ORI_BINS) {
-            uint64_t acc = 0;                             // bin = lane; step q reads bank (q + lane) & 63
+            uint64_t acc = 0;                             // bin = lane; step q reads column (q + lane) mod NC
             for (int q = 0; q < NC; ++q) acc += hp[lane * NC + ((q + lane) & (NC - 1))];
             tf[lane] = vo_hist_fx_to_float(acc);
         }
