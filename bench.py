@@ -16,8 +16,8 @@ and `cpu_baseline` (the CPU oracle on a bounded sample, rank 0 at N=1).
 SIFT, stereo match, tracking, DLT, P3P+MSAC with 2048 hypotheses, landmarks) over
 the KITTI-00 trajectory: 4541 frames rendered at 376x1241 along the reference's
 ground truth (street.py), block-sharded over the ranks with a one-frame halo,
-per-frame records and landmark rows all-gathered, poses chained and landmarks
-moved to the world after the chain; it reports the reference's lagged xz error
+per-frame records all-gathered, poses chained on every rank, each rank's landmark
+rows moved to the world on its device and gathered to rank 0; it reports the reference's lagged xz error
 (PlotOnMap.m:8-20) and ATE against that trajectory (--seq-frames; 0 skips), and
 `large` the 1920x1080 / ~8k keypoint configuration (configs[4]) per GPU with the
 i8-MFMA rate of its dense stereo match block (--large-batch, default 8; 0 skips).
@@ -90,12 +90,12 @@ def launch_ranks(n: int) -> int:
     return p.wait()
 
 
-def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks):
+def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks, gather_over_ranks):
     """KITTI-00 (BASELINE configs[2] at N=1, configs[3] at N=8): frames rendered along the
     reference's ground truth (street.py) into HBM -- each rank only its block + halo -- then
     timed: the sharded VO loop (vo_step_submit_dev / vo_step_collect, 2048 MSAC hypotheses),
-    the all-gathers of per-frame records and camera-frame landmark rows, the pose chain and
-    the landmark world transform.  Accuracy vs the rendered trajectory: PlotOnMap.m:8-20's
+    the all-gather of per-frame records, the pose chain (every rank), the world transform of
+    each rank's own landmark rows on its device and the gather of the world rows to rank 0.  Accuracy vs the rendered trajectory: PlotOnMap.m:8-20's
     lagged xz error and ATE RMSE."""
     from r7020e_visual_odometry_amd import vo, street, kitti, sharding
     gt = street.kitti00_gt()
@@ -122,16 +122,23 @@ def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks)
     dev = torch.device("cuda", local) if dist is not None and dist.get_backend() == "nccl" else None
     barrier()
     t0 = time.perf_counter()
-    outs, X, keep = kitti.run_shard(seq, rank, world, SB, local, n, ctx=ctx)
-    if dist is not None:
-        steps = sharding.gather_steps(outs, n, device=dev)
-        X, keep = sharding.gather_landmark_rows(X, keep, device=dev)
-    else:
-        steps = sharding.steps_of(outs)
-    poses, lm = kitti.assemble(steps, X, keep)
+    outs, _, _ = kitti.run_shard(seq, rank, world, SB, local, n, ctx=ctx, rows_to_host=False)
+    t_loop = time.perf_counter() - t0
+    # the tail: per-frame records all-gathered, chain on every rank, own rows to the world on the
+    # device, world rows gathered to rank 0 only (kitti.finish_shard)
+    tparts = {}
+    poses, steps, lm = kitti.finish_shard(ctx, outs, n, rank, world, local, distributed=dist is not None,
+                                          collective_device=dev, timings=tparts)
     el = time.perf_counter() - t0
+    t_tail = el - t_loop
     barrier()
+    mine = [t_loop, t_tail] + [tparts[k] for k in ("records", "chain", "world", "map")]
+    per_rank = gather_over_ranks(mine)
     el = max_over_ranks(el)
+    t_tail = max_over_ranks(t_tail)
+    n_lm = int(np.asarray(steps["n_landmarks"]).sum())
+    if lm is not None and len(lm) != n_lm:
+        raise RuntimeError(f"landmark map has {len(lm)} rows, the records {n_lm}")
     # per-kernel HIP-event durations of the full path over the block's first PB batches (a
     # separate profiling pass: vo_step_collect synchronises every stream while profiling, so
     # these are the kernels' own durations without the pipeline's overlap), ms per SB frames
@@ -166,12 +173,20 @@ def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks)
     ref_curve = np.loadtxt(ROOT / "data" / "kitti" / "ref_error_digitized.csv", delimiter=",")
     return {"metric": "stereo frames/sec, full per-frame path over the KITTI-00 trajectory (BASELINE configs[2]; configs[3] at 8 GPUs)",
             "value": n / el, "unit": "stereo frames/s", "frames": n, "frames_per_rank": e - s, "batch": SB,
-            "partition": f"block + one-frame halo over {world} rank(s); all-gather of per-frame records and landmark rows",
+            "partition": f"block + one-frame halo over {world} rank(s); all-gather of per-frame records, "
+                         f"landmark world rows gathered to rank 0",
             "rows": street.KITTI_ROWS, "cols": street.KITTI_COLS, "ransac_hypotheses": 2048,
             "frames_with_pose": int(ok.sum()), "mean_inliers": float(steps["n_inliers"][1:].mean()),
             "mean_keypoints_per_image": float((steps["n_left"] + steps["n_right"]).mean() / 2),
             "mean_stereo_matches": float(steps["n_stereo"].mean()), "mean_tracked": float(steps["n_tracked"][1:].mean()),
-            "landmark_rows": int(len(lm)),
+            "landmark_rows": n_lm,
+            "tail_ms": round(t_tail * 1e3, 3),
+            "per_rank_ms": [{"rank": r, "loop": round(v[0] * 1e3, 2), "tail": round(v[1] * 1e3, 3),
+                             "records": round(v[2] * 1e3, 3), "chain": round(v[3] * 1e3, 3),
+                             "world": round(v[4] * 1e3, 3), "map": round(v[5] * 1e3, 3)}
+                            for r, v in enumerate(per_rank)],
+            "tail_note": "max over ranks: records all-gather + chain + own rows to the world on the device + "
+                         "gather of world rows to rank 0 (+ its one D2H of the map)",
             "accuracy": {"lagged_xz_error_m": {"mean": float(err.mean()), "max": float(err.max()), "final": float(err[-1])},
                          "ate_rmse_m": kitti.ate_rmse(poses, gt[:n]),
                          "trajectory_length_m": float(np.linalg.norm(np.diff(gt[:n, :3, 3], axis=0), axis=1).sum()),
@@ -190,7 +205,8 @@ def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks)
             "render_s": render_s,
             "data": "synthetic street world rendered along reference kitti/poses/00.txt with kitti/00/calib.txt P0/P1 "
                     "(KITTI-00 images are not available)",
-            "note": "timed: sharded loop body + gathers + pose chain + landmark world transform; inputs resident in HBM"}
+            "note": "timed: sharded loop body + record all-gather + pose chain + landmark world transform (device) + "
+                    "gather of the world map to rank 0; inputs resident in HBM"}
 
 
 def main():
@@ -252,6 +268,16 @@ def main():
         t = torch.tensor([x], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
+
+    def gather_over_ranks(v) -> list:
+        """Every rank's list of floats (same length), in rank order (reporting only)."""
+        if dist is None:
+            return [list(v)]
+        dev = f"cuda:{local}" if backend == "nccl" else "cpu"
+        t = torch.tensor(v, device=dev, dtype=torch.float64)
+        parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, t)
+        return [p.cpu().tolist() for p in parts]
 
     if world != args.gpus and rank == 0:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}; reporting {world}", file=sys.stderr)
@@ -373,7 +399,7 @@ def main():
     # ---- BASELINE configs[2]/[3]: the full per-frame path over the KITTI-00 trajectory ----
     full = None
     if args.seq_frames > 0:
-        full = sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks)
+        full = sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks, gather_over_ranks)
 
     # ---- BASELINE configs[4]: 1920x1080 synthetic stereo, ~8k keypoints per image, the dense
     # 8k x 8k descriptor block on the i8 matrix cores (k_match_partial) ----

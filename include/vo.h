@@ -32,7 +32,8 @@
  *   vo_step_batch_ex       transpose or conversion (zero-copy MEX gateways)
  *   vo_set_landmark_frame  sharded sequences: camera-frame landmark rows, moved
  *   vo_landmarks_to_world* to the world after the gathered pose chain
- *   vo_chain_poses         (CreateLandmarksFromFeatures.m:17, VO.m:130)
+ *   vo_landmarks_world_dev (CreateLandmarksFromFeatures.m:17, VO.m:130; the
+ *   vo_chain_poses         _dev form on the rank's own rows, on the device)
  *
  * Conventions
  *  - Return value: VO_OK (0) or a negative VO_ERR_* code.  vo_last_error()
@@ -254,9 +255,19 @@ int vo_get_landmarks(vo_ctx* ctx, double* out, int capacity, int* rows);
  * returns it) and keep[rows] (0 = one of the reference's zero rows, :2).  After the chain,
  * vo_landmarks_to_world applies :17 with the frame's world pose; the result equals the
  * world-frame rows a single-process run appends, bit for bit.  Mode 0 (default) = world rows
- * (vo_get_landmarks).  Changing the mode clears the accumulated rows. */
+ * (vo_get_landmarks).  Changing the mode clears the accumulated rows.  Camera-frame rows stay
+ * in device memory; vo_get_landmark_rows copies them to the host. */
 int vo_set_landmark_frame(vo_ctx* ctx, int camera);
 int vo_get_landmark_rows(vo_ctx* ctx, float* X, uint8_t* keep, int capacity, int* rows);
+/* CreateLandmarksFromFeatures.m:17 on the device for the context's own camera-frame rows:
+ * poses[f] (n_frames x 16 row-major double) is the chained world pose of the f-th frame the
+ * context collected since vo_reset / vo_set_landmark_frame (n_frames must equal that count;
+ * frames without rows, e.g. a shard's halo frame, still take a slot).  Writes the world rows
+ * as float32 x, y, z to DEVICE memory d_out [capacity][3] -- the values are single-rounded,
+ * so float32 holds exactly the doubles vo_landmarks_to_world returns; keep = 0 rows are the
+ * reference's zero rows.  *rows = row count (d_out NULL: count only).  Synchronises the
+ * context's stream before returning, so d_out is ready for any other stream (RCCL). */
+int vo_landmarks_world_dev(vo_ctx* ctx, const double* poses, int n_frames, float* d_out, long capacity, long* rows);
 /* Host-only, stateless: out[i] = keep[i] ? single(pose * [X[i]; 1]) : 0 (row-major 4x4 pose). */
 int vo_landmarks_to_world(const double pose[16], const float* X, const uint8_t* keep, int n, double* out);
 /* The same for a whole gathered sequence: frame f's rows_per_frame[f] consecutive rows with

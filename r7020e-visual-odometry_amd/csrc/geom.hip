@@ -928,6 +928,36 @@ void lm_pack_launch(GeomBuffers& g, int B, hipStream_t s)
     VO_LAUNCH(k_lm_pack, dim3(B), dim3(256), 0, s, g.lm_X, g.lm_keep, g.lm_rows, g.kp_cap, g.lm_pX, g.lm_pkeep);
 }
 
+// block f: frame f's rows, one thread per row.  The f64 products and sums are those of the host
+// lm_world (vo_api.hip) in the same order (no contraction: -ffp-contract=off), so the single-rounded
+// world rows equal a single-process run's bit for bit.
+__global__ __launch_bounds__(256) void k_lm_world(const double* __restrict__ poses, const long long* __restrict__ off,
+                                                  const float* __restrict__ X, const uint8_t* __restrict__ keep,
+                                                  float* __restrict__ out)
+{
+    const int f = blockIdx.x;
+    const long long a = off[f], b = off[f + 1];
+    double P[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) P[k] = poses[(size_t)16 * f + k];
+    for (long long r = a + threadIdx.x; r < b; r += 256) {
+        float w[3] = {0.0f, 0.0f, 0.0f};
+        if (keep[r]) {
+            const double x0 = X[3 * r], x1 = X[3 * r + 1], x2 = X[3 * r + 2];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) w[i] = (float)(P[4 * i] * x0 + P[4 * i + 1] * x1 + P[4 * i + 2] * x2 + P[4 * i + 3]);
+        }
+        out[3 * r] = w[0]; out[3 * r + 1] = w[1]; out[3 * r + 2] = w[2];
+    }
+}
+
+void lm_world_launch(const double* poses, const long long* off, int n_frames, const float* X, const uint8_t* keep,
+                     float* out, hipStream_t s)
+{
+    if (n_frames <= 0) return;
+    VO_LAUNCH(k_lm_world, dim3(n_frames), dim3(256), 0, s, poses, off, X, keep, out);
+}
+
 void triangulate_launch(const float* pos, int n, const vo_calib& c, double* X, hipStream_t s)
 {
     if (n <= 0) return;

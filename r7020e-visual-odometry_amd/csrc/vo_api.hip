@@ -133,10 +133,18 @@ struct vo_ctx {
     bool have_features = false;
     double pose[16];
     std::vector<double> landmarks;
-    // camera-frame landmark rows (vo_set_landmark_frame(ctx, 1)): sharded sequences
+    // camera-frame landmark rows (vo_set_landmark_frame(ctx, 1)): sharded sequences.  The rows
+    // stay in device memory (appended by collect from the packed batch rows, a device-to-device
+    // copy on `stream`), so the world transform after the gathered chain runs on the device and
+    // only the world rows move (vo_landmarks_world_dev)
     int lm_camera = 0;
-    std::vector<float> lm_X;
-    std::vector<uint8_t> lm_keep;
+    float* d_lmX = nullptr;                       // [lm_cap][3]
+    uint8_t* d_lmkeep = nullptr;                  // [lm_cap]
+    size_t lm_cap = 0, lm_n = 0;
+    std::vector<long long> lm_frame_off{0};       // row offset of every collected frame (+ end)
+    double* d_lmw_pose = nullptr;                 // vo_landmarks_world_dev staging: poses, offsets
+    long long* d_lmw_off = nullptr;
+    int lmw_cap = 0;
 };
 
 static std::string g_create_err;
@@ -216,6 +224,9 @@ static void destroy_buffers(vo_ctx* c)
     hipFree(c->d_ff[0]); hipFree(c->d_ff[1]); hipFree(c->d_bad);
     hipFree(c->d_fa); hipFree(c->d_fbt); hipFree(c->d_fres);
     hipFree(c->d_fn); hipFree(c->d_mi); hipFree(c->d_mj); hipFree(c->d_mn);
+    hipFree(c->d_lmX); hipFree(c->d_lmkeep); hipFree(c->d_lmw_pose); hipFree(c->d_lmw_off);
+    c->d_lmX = nullptr; c->d_lmkeep = nullptr; c->d_lmw_pose = nullptr; c->d_lmw_off = nullptr;
+    c->lm_cap = 0; c->lmw_cap = 0;
 }
 
 vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib* calib, const vo_sift_params* sift,
@@ -884,7 +895,34 @@ static int collect_batch(vo_ctx* c, vo_step_out* outs, int capacity, int* n_out)
     std::vector<size_t> roff(B + 1, 0);
     for (int f = 0; f < B; ++f) roff[f + 1] = roff[f] + (size_t)std::min(H.rows[f], K);
     total = roff[B];
-    if (total > 0) {
+    if (c->lm_camera) {
+        // camera-frame rows stay on the device: the tracked frames' packed rows are appended to
+        // the store by one device-to-device copy on `stream` (ordered before the next submit of
+        // this set, which reuses the packed buffer)
+        const size_t first = (P.first_tracked ? 0 : roff[1]), add = total - first;
+        if (add > 0) {
+            if (c->lm_n + add > c->lm_cap) {
+                size_t cap = std::max<size_t>({c->lm_n + add, 2 * c->lm_cap, (size_t)1 << 16});
+                float* nX = nullptr; uint8_t* nk = nullptr;
+                if (hipMalloc((void**)&nX, sizeof(float) * 3 * cap) != hipSuccess ||
+                    hipMalloc((void**)&nk, cap) != hipSuccess) {
+                    hipFree(nX);
+                    return fail(c, VO_ERR_HIP, "vo_step_collect: landmark store of %zu rows", cap);
+                }
+                if (c->lm_n > 0) {
+                    HIPC(c, hipMemcpyAsync(nX, c->d_lmX, sizeof(float) * 3 * c->lm_n, hipMemcpyDeviceToDevice, c->stream));
+                    HIPC(c, hipMemcpyAsync(nk, c->d_lmkeep, c->lm_n, hipMemcpyDeviceToDevice, c->stream));
+                }
+                HIPC(c, hipStreamSynchronize(c->stream));
+                hipFree(c->d_lmX); hipFree(c->d_lmkeep);
+                c->d_lmX = nX; c->d_lmkeep = nk; c->lm_cap = cap;
+            }
+            HIPC(c, hipMemcpyAsync(c->d_lmX + 3 * c->lm_n, S.gb->lm_pX + 3 * first, sizeof(float) * 3 * add,
+                                   hipMemcpyDeviceToDevice, c->stream));
+            HIPC(c, hipMemcpyAsync(c->d_lmkeep + c->lm_n, S.gb->lm_pkeep + first, add, hipMemcpyDeviceToDevice, c->stream));
+            c->lm_n += add;
+        }
+    } else if (total > 0) {
         HIPC(c, hipMemcpyAsync(H.pX, S.gb->lm_pX, sizeof(float) * 3 * total, hipMemcpyDeviceToHost, c->copy_stream));
         HIPC(c, hipMemcpyAsync(H.pkeep, S.gb->lm_pkeep, total, hipMemcpyDeviceToHost, c->copy_stream));
         HIPC(c, hipStreamSynchronize(c->copy_stream));
@@ -898,6 +936,10 @@ static int collect_batch(vo_ctx* c, vo_step_out* outs, int capacity, int* n_out)
         o.n_left = H.nkp[2 * f]; o.n_right = H.nkp[2 * f + 1]; o.n_stereo = H.np[f];
         memcpy(o.rel_pose, I4, sizeof(I4));
         const bool tracked = f > 0 || P.first_tracked;
+        if (c->lm_camera) {
+            const size_t r = tracked ? roff[f + 1] - roff[f] : 0;
+            c->lm_frame_off.push_back(c->lm_frame_off.back() + (long long)r);
+        }
         if (tracked) {
             o.status = H.fg[f].status;
             o.n_tracked = H.fg[f].n_tracked;
@@ -910,10 +952,7 @@ static int collect_batch(vo_ctx* c, vo_step_out* outs, int capacity, int* n_out)
             const float* Xf = H.pX + roff[f] * 3;
             const uint8_t* kf = H.pkeep + roff[f];
             o.n_landmarks = r;
-            if (c->lm_camera) {
-                c->lm_X.insert(c->lm_X.end(), Xf, Xf + (size_t)r * 3);
-                c->lm_keep.insert(c->lm_keep.end(), kf, kf + r);
-            } else {
+            if (!c->lm_camera) {
                 size_t base = c->landmarks.size();
                 c->landmarks.resize(base + (size_t)r * 3, 0.0);
                 for (int m = 0; m < r; ++m)
@@ -1045,8 +1084,8 @@ int vo_set_landmark_frame(vo_ctx* c, int camera)
     if (!c->pending.empty()) return fail(c, VO_ERR_STATE, "vo_set_landmark_frame: batches pending");
     c->lm_camera = camera;
     c->landmarks.clear();
-    c->lm_X.clear();
-    c->lm_keep.clear();
+    c->lm_n = 0;
+    c->lm_frame_off.assign(1, 0);
     return VO_OK;
 }
 
@@ -1054,12 +1093,51 @@ int vo_get_landmark_rows(vo_ctx* c, float* X, uint8_t* keep, int capacity, int* 
 {
     if (!c || capacity < 0) return fail(c, VO_ERR_ARG, "vo_get_landmark_rows: bad arguments");
     if (!c->lm_camera) return fail(c, VO_ERR_STATE, "vo_get_landmark_rows: context keeps world rows (vo_set_landmark_frame(ctx, 1) first)");
-    const int r = (int)c->lm_keep.size();
+    if (!c->pending.empty()) return fail(c, VO_ERR_STATE, "vo_get_landmark_rows: batches pending");
+    const int r = (int)c->lm_n;
     if (rows) *rows = r;
     const int m = std::min(r, capacity);
-    if (X && m > 0) memcpy(X, c->lm_X.data(), sizeof(float) * 3 * m);
-    if (keep && m > 0) memcpy(keep, c->lm_keep.data(), m);
+    if (m > 0 && (X || keep)) {
+        hipSetDevice(c->device);
+        HIPC(c, hipStreamSynchronize(c->stream));
+        if (X) HIPC(c, hipMemcpy(X, c->d_lmX, sizeof(float) * 3 * m, hipMemcpyDeviceToHost));
+        if (keep) HIPC(c, hipMemcpy(keep, c->d_lmkeep, m, hipMemcpyDeviceToHost));
+    }
     return r > capacity && (X || keep) ? fail(c, VO_ERR_CAPACITY, "vo_get_landmark_rows: %d rows exceed capacity %d", r, capacity) : VO_OK;
+}
+
+int vo_landmarks_world_dev(vo_ctx* c, const double* poses, int n_frames, float* d_out, long capacity, long* rows)
+{
+    if (!c || n_frames < 0 || capacity < 0 || (n_frames > 0 && !poses))
+        return fail(c, VO_ERR_ARG, "vo_landmarks_world_dev: bad arguments");
+    if (!c->lm_camera) return fail(c, VO_ERR_STATE, "vo_landmarks_world_dev: context keeps world rows (vo_set_landmark_frame(ctx, 1) first)");
+    if (!c->pending.empty()) return fail(c, VO_ERR_STATE, "vo_landmarks_world_dev: batches pending");
+    const int nf = (int)c->lm_frame_off.size() - 1;
+    if (n_frames != nf)
+        return fail(c, VO_ERR_ARG, "vo_landmarks_world_dev: %d poses for %d collected frames", n_frames, nf);
+    const long r = (long)c->lm_n;
+    if (rows) *rows = r;
+    if (r == 0) return VO_OK;
+    if (!d_out) return VO_OK;
+    if (r > capacity) return fail(c, VO_ERR_CAPACITY, "vo_landmarks_world_dev: %ld rows exceed capacity %ld", r, capacity);
+    hipSetDevice(c->device);
+    if (nf > c->lmw_cap) {
+        hipFree(c->d_lmw_pose); hipFree(c->d_lmw_off);
+        c->d_lmw_pose = nullptr; c->d_lmw_off = nullptr; c->lmw_cap = 0;
+        const int cap = std::max(nf, 1024);
+        HIPC(c, hipMalloc((void**)&c->d_lmw_pose, sizeof(double) * 16 * cap));
+        HIPC(c, hipMalloc((void**)&c->d_lmw_off, sizeof(long long) * (cap + 1)));
+        c->lmw_cap = cap;
+    }
+    HIPC(c, hipMemcpyAsync(c->d_lmw_pose, poses, sizeof(double) * 16 * nf, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(c->d_lmw_off, c->lm_frame_off.data(), sizeof(long long) * (nf + 1), hipMemcpyHostToDevice,
+                           c->stream));
+    lm_world_launch(c->d_lmw_pose, c->d_lmw_off, nf, c->d_lmX, c->d_lmkeep, d_out, c->stream);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(c, VO_ERR_HIP, "launch: %s", hipGetErrorString(e));
+    // d_out is read by the caller's streams (torch, RCCL) next: complete before returning
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return VO_OK;
 }
 
 int vo_landmarks_to_world(const double pose[16], const float* X, const uint8_t* keep, int n, double* out)
@@ -1114,8 +1192,8 @@ int vo_reset(vo_ctx* c)
     c->frame_index = 0;
     memcpy(c->pose, I4, sizeof(I4));
     c->landmarks.clear();
-    c->lm_X.clear();
-    c->lm_keep.clear();
+    c->lm_n = 0;
+    c->lm_frame_off.assign(1, 0);
     HIPC(c, hipMemset(c->d_pair_n + c->max_batch, 0, sizeof(int)));
     HIPC(c, hipMemset(c->aux.pair_n + c->max_batch, 0, sizeof(int)));
     return VO_OK;

@@ -88,6 +88,12 @@ static inline int* track_list(const GeomBuffers& g, int f, int l) { return g.lis
 // Pack frames [0, B)'s landmark rows contiguously into lm_pX / lm_pkeep.
 void lm_pack_launch(GeomBuffers& g, int B, hipStream_t s);
 
+// CreateLandmarksFromFeatures.m:17 on the device for a run of frames: frame f's rows
+// [off[f], off[f+1]) of the camera-frame store (X [rows][3], keep [rows]) go to the world with
+// poses[f] (row-major 4x4, f64), rounded through single into out [rows][3] (zero rows for keep 0).
+void lm_world_launch(const double* poses, const long long* off, int n_frames, const float* X, const uint8_t* keep,
+                     float* out, hipStream_t s);
+
 // Standalone launchers used by the single-call ABI functions (frame slot 0).
 // pos: [n][4] (x1, y1, x2, y2) device floats.
 void triangulate_launch(const float* pos, int n, const vo_calib& c, double* X, hipStream_t s);

@@ -333,13 +333,15 @@ def _local_device() -> int:
 
 
 def run_shard(seq, rank: int, world: int, batch: int = 16, device: int | None = None,
-              stop: int | None = None, ctx=None):
+              stop: int | None = None, ctx=None, rows_to_host: bool = True):
     """One rank's part of a frame-sharded run (`sharding.py`): the block
     [start, end) of frames plus a one-frame halo, MSAC keyed by the global frame index,
     landmark rows kept in the camera frame.  `seq` is a KittiSequence (PNG frames) or a
     (L, R) pair of device tensors [n, H, W] holding the whole sequence (or at least
     frames [halo, end)).  Returns (outs: the block's STEP_DTYPE records [end - start],
-    X [L, 3] float32, keep [L] bool: the block's camera-frame landmark rows)."""
+    X [L, 3] float32, keep [L] bool: the block's camera-frame landmark rows).  With
+    rows_to_host=False (and a caller-owned `ctx`) the rows stay in the context's device store
+    for `finish_shard` and X, keep are None."""
     import torch
     from . import sharding, vo
     device = _local_device() if device is None else device
@@ -357,7 +359,9 @@ def run_shard(seq, rank: int, world: int, batch: int = 16, device: int | None = 
     ctx.set_frame_index(h)
     src = device_batches(seq[0], seq[1], batch, h, e) if on_device else seq.batches(batch, h, e)
     outs = _pipelined(ctx, src, torch.device("cuda", device))
-    X, keep = ctx.get_landmark_rows()
+    if not rows_to_host and own:
+        raise ValueError("run_shard: rows_to_host=False needs a caller-owned ctx (the rows live in it)")
+    X, keep = ctx.get_landmark_rows() if rows_to_host else (None, None)
     if own:
         ctx.close()
     outs = np.concatenate(outs) if outs else np.zeros(0, vo.STEP_DTYPE)
@@ -390,25 +394,74 @@ def assemble(steps: dict, X: np.ndarray, keep: np.ndarray, to_world=None):
     return poses, lm
 
 
+def finish_shard(ctx, outs, n: int, rank: int, world: int, device: int, group=None, distributed: bool = True,
+                 collective_device=None, timings: dict | None = None):
+    """The tail of a frame-sharded run after `run_shard(..., rows_to_host=False)` (SURVEY §8(e)
+    step 4-5, `sharding.py`):
+      1. one all-gather of the per-frame records (relative pose, status, counts: 23 doubles per
+         frame) -- skipped with distributed=False (one process);
+      2. every rank chains the world poses itself (VO.m:130, libvo vo_chain_poses);
+      3. every rank moves its OWN camera-frame rows to the world on the device with its frames'
+         chained poses (CreateLandmarksFromFeatures.m:17, vo_landmarks_world_dev);
+      4. the world rows go to rank 0 only (one dist.gather; RCCL from device buffers when
+         collective_device is the rank's GPU, CPU tensors for gloo).
+    Returns (world poses [n, 4, 4], gathered per-frame records, landmarks float32 [L, 3] on rank 0
+    -- single-rounded values, equal to a single-process run's rows -- and None on other ranks).
+    `timings` (a dict) receives the seconds of each step: records, chain, world (device
+    transform), map (gather to rank 0 + its copy to the host)."""
+    import time
+    import torch
+    from . import sharding, vo
+    tm = timings if timings is not None else {}
+    t0 = time.perf_counter()
+    steps = sharding.gather_steps(outs, n, group=group, device=collective_device) if distributed \
+        else sharding.steps_of(outs)
+    t1 = time.perf_counter()
+    poses = vo.chain_poses(steps["rel_pose"], steps["status"])
+    t2 = time.perf_counter()
+    counts = sharding.rank_row_counts(steps["n_landmarks"], n, world)
+    s, e = sharding.shard_range(n, world, rank)
+    h = sharding.halo_start(s)
+    m = max(max(counts), 1)
+    buf = torch.empty((m, 3), dtype=torch.float32, device=torch.device("cuda", device))
+    rows = ctx.landmarks_world_dev(poses[h:e], buf.data_ptr(), m)
+    if rows != counts[rank]:
+        raise RuntimeError(f"rank {rank}: {rows} landmark rows on the device, records say {counts[rank]}")
+    t3 = time.perf_counter()
+    if not distributed:
+        lm = buf[:rows].cpu().numpy()
+    else:
+        lm = sharding.gather_rows_to_root(buf if collective_device is not None else buf[:rows].cpu(), counts,
+                                          group=group, device=collective_device)
+    tm.update(records=t1 - t0, chain=t2 - t1, world=t3 - t2, map=time.perf_counter() - t3)
+    return poses, steps, lm
+
+
 def run_distributed(seq, batch: int = 16, device: int | None = None, stop: int | None = None,
                     group=None):
     """Frame-sharded run over a torch.distributed group (one process per GPU; RCCL over
-    xGMI with the nccl backend): every rank runs its block (`run_shard`), one all-gather of
-    the per-frame records (relative pose, status, counts) and one of the camera-frame
-    landmark rows, then the world-pose chain (host product of `VO.m:130`) and the landmark
-    world transform (`CreateLandmarksFromFeatures.m:17`).  Returns (world poses [n, 4, 4],
-    gathered per-frame records, landmarks [L, 3]) on every rank, equal bit for bit to a
-    single-process run."""
+    xGMI with the nccl backend): every rank runs its block (`run_shard`, landmark rows kept on
+    the device), then `finish_shard`: one all-gather of the per-frame records, the world-pose
+    chain on every rank (host product of `VO.m:130`), each rank's own rows moved to the world on
+    its device (`CreateLandmarksFromFeatures.m:17`) and gathered to rank 0.  Returns (world
+    poses [n, 4, 4], gathered per-frame records, landmarks float32 [L, 3] on rank 0 / None on the
+    other ranks), equal bit for bit to a single-process run."""
     import torch
     import torch.distributed as dist
-    from . import sharding
+    from . import sharding, vo
     device = _local_device() if device is None else device
     n_all = seq[0].shape[0] if isinstance(seq, tuple) else len(seq)
     n = n_all if stop is None else min(stop, n_all)
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    outs, X, keep = run_shard(seq, rank, world, batch, device, n)
-    dev = torch.device("cuda", device) if dist.get_backend(group) == "nccl" else None
-    steps = sharding.gather_steps(outs, n, group=group, device=dev)
-    Xg, kg = sharding.gather_landmark_rows(X, keep, group=group, device=dev)
-    poses, lm = assemble(steps, Xg, kg)
-    return poses, steps, lm
+    if isinstance(seq, tuple):
+        rows, cols = seq[0].shape[1], seq[0].shape[2]
+    else:
+        rows, cols = seq.rows, seq.cols
+    P1, P2 = seq_calib(seq)
+    ctx = vo.Context(rows, cols, batch, device=device, calib=vo.calib_from(P1, P2))
+    try:
+        outs, _, _ = run_shard(seq, rank, world, batch, device, n, ctx=ctx, rows_to_host=False)
+        dev = torch.device("cuda", device) if dist.get_backend(group) == "nccl" else None
+        return finish_shard(ctx, outs, n, rank, world, device, group=group, collective_device=dev)
+    finally:
+        ctx.close()

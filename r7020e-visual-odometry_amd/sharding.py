@@ -16,10 +16,13 @@ for bit.
 The landmark map: CreateLandmarksFromFeatures.m:17 moves a
 frame's new points into the world with that frame's pose, which a rank that
 starts mid-sequence only knows after the chain.  Ranks therefore keep their rows
-in the camera frame (libvo vo_set_landmark_frame), the rows are all-gathered in
-frame order (`gather_landmark_rows`), and `world_landmarks` applies :17 per frame
-with the chained pose -- the same rows, bit for bit, that a single process
-appends.
+in the camera frame (libvo vo_set_landmark_frame; the rows stay in device memory).
+Only the per-frame records are all-gathered (23 doubles per frame); every rank
+chains the poses itself, moves its OWN rows to the world with its frames' chained
+poses (on the device: libvo vo_landmarks_world_dev; `world_landmarks` is the
+host form), and the world rows go to rank 0 alone (`gather_rows_to_root`, one
+dist.gather: RCCL from device buffers).  The per-rank tail is thus proportional to
+the rank's own rows, and the result equals a single process's rows bit for bit.
 """
 from __future__ import annotations
 
@@ -112,27 +115,42 @@ def steps_of(outs) -> dict:
     return out
 
 
-def gather_landmark_rows(X_local: np.ndarray, keep_local: np.ndarray, group=None, device=None):
-    """All-gather the camera-frame landmark rows of every rank (rank order = frame order)
-    -> (X [L, 3] float32, keep [L] bool).  Two collectives: the row counts, then the rows
-    padded to the largest count (float32 x, y, z, keep: exact)."""
+def rank_row_counts(n_landmarks, n_frames: int, world: int) -> list[int]:
+    """Landmark rows each rank's block appends (the gathered per-frame n_landmarks summed over
+    every rank's `shard_range`): every rank knows every rank's count without a collective."""
+    n_landmarks = np.asarray(n_landmarks, np.int64)
+    return [int(n_landmarks[slice(*shard_range(n_frames, world, r))].sum()) for r in range(world)]
+
+
+def gather_rows_to_root(rows_local, counts, group=None, device=None):
+    """Rank 0 of the group receives every rank's world landmark rows (float32 [counts[r], 3], rank
+    order = frame order) as one host array; the other ranks get None.  One dist.gather of
+    buffers padded to max(counts): with device=<cuda device> the buffers stay on the device
+    (RCCL over xGMI; `rows_local` may already be such a tensor of at least max(counts) rows), with
+    device=None they are CPU tensors (gloo).  Only rank 0 copies rows to the host."""
     import torch
     import torch.distributed as dist
-    world = dist.get_world_size(group)
-    n = torch.tensor([len(keep_local)], dtype=torch.int64, device=device)
-    counts = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(counts, n, group=group)
-    counts = [int(c.item()) for c in counts]
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    if len(counts) != world:
+        raise ValueError(f"{len(counts)} row counts for a world of {world}")
     m = max(max(counts), 1)
-    buf = torch.zeros((m, 4), dtype=torch.float32, device=device)
-    if len(keep_local):
-        loc = np.concatenate([np.asarray(X_local, np.float32).reshape(-1, 3),
-                              np.asarray(keep_local, np.float32).reshape(-1, 1)], 1)
-        buf[: len(loc)] = torch.from_numpy(loc).to(buf.device)
+    dev = torch.device("cpu") if device is None else torch.device(device)
+    if torch.is_tensor(rows_local) and rows_local.device == dev and rows_local.dtype == torch.float32 \
+            and rows_local.dim() == 2 and rows_local.shape[0] >= m and rows_local.shape[1] == 3:
+        buf = rows_local[:m]
+    else:
+        loc = rows_local if torch.is_tensor(rows_local) else torch.from_numpy(np.asarray(rows_local, np.float32))
+        loc = loc.reshape(-1, 3)[: counts[rank]]
+        buf = torch.zeros((m, 3), dtype=torch.float32, device=dev)
+        buf[: loc.shape[0]] = loc.to(dev)
+    buf = buf.contiguous()
+    dst = 0 if group is None else dist.get_global_rank(group, 0)
+    if rank != 0:
+        dist.gather(buf, None, dst=dst, group=group)
+        return None
     parts = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(parts, buf, group=group)
-    rows = np.concatenate([parts[r][: counts[r]].cpu().numpy() for r in range(world)])
-    return rows[:, :3].copy(), rows[:, 3] != 0
+    dist.gather(buf, parts, dst=dst, group=group)
+    return torch.cat([p[:c] for p, c in zip(parts, counts)]).cpu().numpy()
 
 
 def world_landmarks(poses: np.ndarray, n_landmarks: np.ndarray, X: np.ndarray, keep: np.ndarray,

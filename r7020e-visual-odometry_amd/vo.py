@@ -92,7 +92,7 @@ EXPORTS = [
     "vo_sift_match_batch_dev", "vo_fetch_keypoints", "vo_fetch_stereo_pairs", "vo_fetch_gaussian", "vo_stream", "vo_set_profiling",
     "vo_kernel_times", "vo_set_frame_index", "vo_set_concurrency",
     "vo_set_landmark_frame", "vo_get_landmark_rows", "vo_landmarks_to_world", "vo_match_f32",
-    "vo_sift_ex", "vo_step_batch_ex", "vo_chain_poses", "vo_landmarks_to_world_frames",
+    "vo_sift_ex", "vo_step_batch_ex", "vo_chain_poses", "vo_landmarks_to_world_frames", "vo_landmarks_world_dev",
 ]
 
 # the test build (csrc `make exp`, -DVO_EXPERIMENTAL=1): libvo plus the experimental kernels kept
@@ -172,6 +172,7 @@ def load_library(path: str | os.PathLike | None = None):
     L.vo_landmarks_to_world_frames.argtypes = [P(C.c_double), P(C.c_int32), C.c_int, P(C.c_float), P(C.c_uint8), C.c_long,
                                                P(C.c_double)]
     L.vo_chain_poses.argtypes = [P(C.c_double), P(C.c_int32), C.c_int, P(C.c_double), P(C.c_double)]
+    L.vo_landmarks_world_dev.argtypes = [vp, P(C.c_double), C.c_int, vp, C.c_long, P(C.c_long)]
     L.vo_kernel_times.argtypes = [vp, P(C.c_char_p), P(C.c_double), P(C.c_int), C.c_int, P(C.c_int)]
     _libs[key] = L
     return L
@@ -478,6 +479,23 @@ class Context:
         self._check(self.lib.vo_get_landmark_rows(self.h, _p(X, C.c_float), _p(keep, C.c_uint8), rows.value,
                                                   C.byref(rows)))
         return X[: rows.value].copy(), keep[: rows.value].astype(bool)
+
+    def landmark_row_count(self) -> int:
+        """Camera-frame landmark rows held on the device (vo_set_landmark_frame(ctx, 1))."""
+        rows = C.c_int(0)
+        self._check(self.lib.vo_get_landmark_rows(self.h, None, None, 0, C.byref(rows)))
+        return rows.value
+
+    def landmarks_world_dev(self, poses, d_out: int, capacity: int) -> int:
+        """CreateLandmarksFromFeatures.m:17 on the device (vo_landmarks_world_dev): the context's
+        camera-frame rows moved to the world with poses[f], the chained world pose of its f-th
+        collected frame, written as float32 [rows, 3] to device memory at d_out (e.g. a torch
+        tensor's data_ptr(), `capacity` rows).  Returns the row count; d_out is ready on return."""
+        P = np.ascontiguousarray(poses, np.float64).reshape(-1, 16)
+        rows = C.c_long(0)
+        self._check(self.lib.vo_landmarks_world_dev(self.h, _p(P, C.c_double), P.shape[0], C.c_void_p(d_out or None),
+                                                    int(capacity), C.byref(rows)))
+        return rows.value
 
     def reset(self):
         self._check(self.lib.vo_reset(self.h))

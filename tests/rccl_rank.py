@@ -5,8 +5,9 @@ The group is created FIRST -- `dist.init_process_group("nccl", device_id=cuda:0)
 rendezvous (MASTER_ADDR/MASTER_PORT/RANK/WORLD_SIZE set by the parent) before any other GPU
 work -- exactly as bench.py's ranks do.  Then a KITTI-00 stretch rendered along the reference's
 ground truth (street.py) runs through the sharded path with the collectives on device tensors
-(sharding.gather_steps / gather_landmark_rows with device=cuda, i.e. RCCL), and through a plain
-single-process libvo run; rank 0 prints one JSON line comparing the two (VO.m:130-134 chain,
+(kitti.finish_shard with collective_device=cuda: the records all-gather and the gather of the
+device-transformed world rows to rank 0 run through RCCL), and through a plain single-process libvo
+run; rank 0 prints one JSON line comparing the two (VO.m:130-134 chain,
 CreateLandmarksFromFeatures.m:17 map)."""
 import json
 import os
@@ -27,7 +28,7 @@ def main():
     dist.init_process_group("nccl", device_id=dev)
     rank, world = dist.get_rank(), dist.get_world_size()
     import vo_amd  # noqa: F401
-    from r7020e_visual_odometry_amd import kitti, sharding, street, vo
+    from r7020e_visual_odometry_amd import kitti, street, vo
     frames = range(int(os.environ.get("VO_RCCL_FIRST", "2000")), int(os.environ.get("VO_RCCL_LAST", "2009")))
     n = len(frames)
     gt = street.kitti00_gt()
@@ -38,10 +39,10 @@ def main():
     torch.cuda.synchronize()
     B = 3
     # the sharded path, collectives on device tensors (RCCL)
-    outs, X, keep = kitti.run_shard((L, R, P0, P1), rank, world, B, local, n)
-    steps = sharding.gather_steps(outs, n, device=dev)
-    Xg, keepg = sharding.gather_landmark_rows(X, keep, device=dev)
-    poses, lm = kitti.assemble(steps, Xg, keepg)
+    sctx = vo.Context(street.KITTI_ROWS, street.KITTI_COLS, B, device=local, calib=vo.calib_from(P0, P1))
+    outs, _, _ = kitti.run_shard((L, R, P0, P1), rank, world, B, local, n, ctx=sctx, rows_to_host=False)
+    poses, steps, lm = kitti.finish_shard(sctx, outs, n, rank, world, local, collective_device=dev)
+    sctx.close()
     t = torch.tensor([float(rank) + 0.25], device=dev, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)                    # bench.py's max_over_ranks
     maxv = float(t.item())
@@ -55,7 +56,8 @@ def main():
            "rel_equal": bool(np.array_equal(steps["rel_pose"], ref["rel_pose"])),
            "status_equal": bool(np.array_equal(steps["status"], ref["status"].astype(np.int64))),
            "n_landmarks_equal": bool(np.array_equal(steps["n_landmarks"], ref["n_landmarks"].astype(np.int64))),
-           "landmarks_equal": bool(lm.shape == lm1.shape and np.array_equal(lm, lm1)),
+           "landmarks_equal": bool(lm is not None and lm.dtype == np.float32 and lm.shape == lm1.shape
+                                   and np.array_equal(lm.astype(np.float64), lm1)),
            "landmark_rows": int(len(lm1)), "frames_with_pose": int((ref["status"][1:] == 0).sum()),
            "max_over_ranks": maxv}
     dist.barrier()

@@ -40,8 +40,13 @@ def image_divergence(oracle, img):
     kc, dc = oracle.sift(img, cv=True)
     si, ci = match_keypoints(ks, kc)
     agree = len(si) / max(len(ks), len(kc), 1)
+    # the spec keeps exact duplicates (same x, y, octave, layer, angle) that OpenCV's
+    # removeDuplicatedSorted drops: agreement net of that one documented difference
+    uniq = len({(float(k["x"]), float(k["y"]), int(k["octave"]), int(k["layer"]), float(k["angle"])) for k in ks})
+    agree_dedup = len(si) / max(uniq, len(kc), 1)
     diff = np.abs(ds[si].astype(np.int32) - dc[ci].astype(np.int32)).max(axis=1) if len(si) else np.zeros(1)
-    return {"n_spec": len(ks), "n_cv": len(kc), "agreement": agree,
+    return {"n_spec": len(ks), "n_spec_unique": uniq, "n_cv": len(kc), "agreement": agree,
+            "agreement_dedup": agree_dedup, "cv_unmatched": len(kc) - len(ci),
             "desc_linf_max": int(diff.max()), "desc_linf_p99": float(np.percentile(diff, 99)),
             "desc_linf_mean": float(diff.mean())}, (ks, ds, kc, dc, si, ci)
 

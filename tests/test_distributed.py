@@ -1,10 +1,11 @@
 """Multi-rank path on CPU (gloo): a sequence is block-sharded with a one-frame halo,
 each rank runs its frames (through the CPU oracle, standing in for its GPU: these
-ranks are libvo-free), the per-frame records and the camera-frame landmark rows are
-all-gathered, the relative poses are chained and the landmark rows moved to the world
-with their frame's chained pose (CreateLandmarksFromFeatures.m:17).
-World poses AND the landmark map equal the single-process run bit for bit (MSAC keys
-are global frame indices)."""
+ranks are libvo-free), the per-frame records are all-gathered, every rank chains the
+relative poses and moves its OWN landmark rows to the world with its frames' chained
+poses (CreateLandmarksFromFeatures.m:17), and the world rows are
+gathered to rank 0 only (the shape of kitti.finish_shard).  World poses (on every rank)
+AND the landmark map (rank 0) equal the single-process run bit for bit (MSAC keys are
+global frame indices); the other ranks hold no map."""
 import os
 import socket
 import sys
@@ -31,7 +32,7 @@ def _worker(rank, world, port, path, result_q):
     import torch
     import torch.distributed as dist
     import vo_amd  # noqa: F401
-    from r7020e_visual_odometry_amd import sharding, kitti
+    from r7020e_visual_odometry_amd import sharding
     import oracle
     torch.set_num_threads(1)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -45,10 +46,16 @@ def _worker(rank, world, port, path, result_q):
     outs, (X, keep) = oracle.run_sequence(L[h:e], R[h:e], z["P1"], z["P2"], key0=h, camera_rows=True)
     outs = outs[s - h:]                                  # drop the halo frame
     steps = sharding.gather_steps(outs, n)
-    Xg, kg = sharding.gather_landmark_rows(X, keep)
-    poses, lm = kitti.assemble(steps, Xg, kg, to_world=oracle.landmarks_to_world)
+    poses = sharding.chain(steps["rel_pose"], status=steps["status"])
+    counts = sharding.rank_row_counts(steps["n_landmarks"], n, world)
+    assert counts[rank] == len(keep)
+    own = sharding.world_landmarks(poses[s:e], steps["n_landmarks"][s:e], X, keep, oracle.landmarks_to_world)
+    assert np.array_equal(own.astype(np.float32).astype(np.float64), own)     # single-rounded: float32 is exact
+    lm = sharding.gather_rows_to_root(own.astype(np.float32), counts)
     if rank == 0:
         result_q.put((steps, poses, lm))
+    else:
+        assert lm is None
     dist.barrier()
     dist.destroy_process_group()
 
@@ -73,7 +80,7 @@ def _check(res, ref_outs, ref_lm):
     for k in ("status", "n_left", "n_right", "n_stereo", "n_tracked", "n_inliers", "n_landmarks"):
         assert np.array_equal(steps[k], ref_outs[k]), k
     assert np.array_equal(poses, ref_outs["pose"])
-    assert lm.shape == ref_lm.shape and np.array_equal(lm, ref_lm)
+    assert lm.dtype == np.float32 and lm.shape == ref_lm.shape and np.array_equal(lm.astype(np.float64), ref_lm)
 
 
 def test_two_rank_sharded_golden_sequence_equals_single_process(tmp_path):

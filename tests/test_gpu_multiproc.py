@@ -2,7 +2,8 @@
 ever run the oracle per rank).  Two spawned ranks on this box's one GPU (gloo for the
 collectives; the 8-GPU runs use nccl = RCCL) run kitti.run_distributed over a KITTI-00 stretch
 rendered along the reference's ground truth; world poses, per-frame records and the landmark
-map equal a single-process libvo run bit for bit."""
+map (transformed on each rank's device, gathered to rank 0) equal a single-process libvo run bit
+for bit."""
 import os
 import socket
 import sys
@@ -38,6 +39,8 @@ def _rank(rank, world, port, path, q):
     poses, steps, lm = kitti.run_distributed((L, R, z["P0"], z["P1"]), batch=2, device=0)
     if rank == 0:
         q.put((poses, steps["rel_pose"], steps["n_landmarks"], lm))
+    else:
+        assert lm is None                                   # the map is gathered to rank 0 only
     dist.barrier()
     dist.destroy_process_group()
 
@@ -68,4 +71,4 @@ def test_two_process_group_libvo_equals_single_process(vo, tmp_path):
         assert p.exitcode == 0
     assert np.array_equal(poses, outs["pose"]) and np.array_equal(rel, outs["rel_pose"])
     assert np.array_equal(nlm, outs["n_landmarks"])
-    assert lm.shape == lm1.shape and np.array_equal(lm, lm1)
+    assert lm.dtype == np.float32 and lm.shape == lm1.shape and np.array_equal(lm.astype(np.float64), lm1)

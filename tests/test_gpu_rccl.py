@@ -1,7 +1,8 @@
 """RCCL on the hardware: a real `nccl` (= RCCL) process group on the GPU,
 world size 1, env rendezvous on 127.0.0.1 -- the branch bench.py's ranks take -- runs the
-sharded sequence path with its all-gathers on device tensors (sharding.gather_steps,
-gather_landmark_rows with device=cuda) and the max-over-ranks all-reduce; the gathered
+sharded sequence path with its collectives on device tensors (kitti.finish_shard: the records
+all-gather, the gather of device-transformed world rows to rank 0) and the max-over-ranks
+all-reduce; the gathered
 trajectory (VO.m:130-134) and landmark map (CreateLandmarksFromFeatures.m:17) equal a plain
 single-process libvo run bit for bit.  The rank runs in a child process (tests/rccl_rank.py)
 so that the process group is created before any other GPU work, as in bench.py."""

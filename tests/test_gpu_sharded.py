@@ -76,6 +76,43 @@ def test_sharded_libvo_equals_single_run(vo, street_seq, single_run, world):
     assert lm.shape == lm1.shape and np.array_equal(lm, lm1)
 
 
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_device_world_transform_of_shards_equals_single_run(vo, street_seq, single_run, world):
+    """kitti.finish_shard's per-rank step: each shard's own rows moved to the world on the device
+    (vo_landmarks_world_dev, k_lm_world) with the chained poses of its frames, halo frame
+    included; the shards' float32 rows concatenated in rank order equal the single run's map."""
+    import torch
+    from r7020e_visual_odometry_amd import kitti, sharding
+    L, R, P0, P1, _ = street_seq
+    outs1, lm1 = single_run
+    n = L.shape[0]
+    seq = (L, R, P0, P1)
+    ctx = vo.Context(ROWS, COLS, 3, calib=vo.calib_from(P0, P1))
+    outs = [kitti.run_shard(seq, r, world, 3, 0, ctx=ctx, rows_to_host=False)[0] for r in range(world)]
+    steps = sharding.steps_of(np.concatenate(outs))
+    poses = vo.chain_poses(steps["rel_pose"], steps["status"])
+    assert np.array_equal(poses, outs1["pose"])
+    counts = sharding.rank_row_counts(steps["n_landmarks"], n, world)
+    parts = []
+    for r in range(world):                       # each "rank" again, its rows left on the device
+        kitti.run_shard(seq, r, world, 3, 0, ctx=ctx, rows_to_host=False)
+        s, e = sharding.shard_range(n, world, r)
+        h = sharding.halo_start(s)
+        assert ctx.landmarks_world_dev(poses[h:e], 0, 0) == counts[r]          # count only
+        buf = torch.full((counts[r] + 5, 3), float("nan"), device="cuda:0")
+        assert ctx.landmarks_world_dev(poses[h:e], buf.data_ptr(), buf.shape[0]) == counts[r]
+        assert torch.isnan(buf[counts[r]:]).all()                                # nothing past the rows
+        parts.append(buf[: counts[r]].cpu().numpy())
+        with pytest.raises(vo.VOError):                                         # one pose per collected frame
+            ctx.landmarks_world_dev(poses[h:e - 1], buf.data_ptr(), buf.shape[0])
+        if counts[r]:
+            with pytest.raises(vo.VOError):                                     # capacity
+                ctx.landmarks_world_dev(poses[h:e], buf.data_ptr(), counts[r] - 1)
+    ctx.close()
+    lm = np.concatenate(parts)
+    assert lm.shape == lm1.shape and np.array_equal(lm.astype(np.float64), lm1)
+
+
 def test_camera_frame_rows_transform_to_world_rows(vo, street_seq, single_run):
     """vo_set_landmark_frame(1) + vo_landmarks_to_world == the world rows of mode 0."""
     from r7020e_visual_odometry_amd import kitti, sharding

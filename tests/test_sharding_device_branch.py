@@ -1,9 +1,10 @@
-"""The nccl (RCCL) branch of the sharding gathers, on the CPU with a spy in place of
-torch.distributed: with device=<dev> every tensor handed to all_gather is built on that device
-(RCCL only takes device tensors), records and landmark rows come back in frame order from a
-3-rank world, and the results are read back through .cpu().  The spy's device is the CPU (no
-GPU here); what is checked is that the helpers place every collective buffer on the device they
-are given, never on a default one (bench.py passes cuda:LOCAL_RANK under nccl)."""
+"""The nccl (RCCL) branch of the sharding collectives, on the CPU with a spy in place of
+torch.distributed: with device=<dev> every tensor handed to all_gather / gather is built on that
+device (RCCL only takes device tensors), records come back in frame order from a 3-rank world,
+world landmark rows reach rank 0 only (in rank = frame order, padding dropped), and the results
+are read back through .cpu().  The spy's device is the CPU (no GPU here); what is checked is that
+the helpers place every collective buffer on the device they are given, never on a default one
+(bench.py passes cuda:LOCAL_RANK under nccl)."""
 import types
 
 import numpy as np
@@ -23,6 +24,19 @@ class SpyDist(types.SimpleNamespace):
     def get_world_size(self, group=None):
         return self.world
 
+    def get_rank(self, group=None):
+        return self.rank
+
+    def gather(self, t, gather_list=None, dst=0, group=None):
+        self.calls.append((t.device, t.dtype, tuple(t.shape)))
+        if self.rank != dst:
+            assert gather_list is None
+            return
+        assert len(gather_list) == self.world
+        for r in range(self.world):
+            assert gather_list[r].device == t.device and gather_list[r].shape == t.shape
+            gather_list[r].copy_(t if r == self.rank else self.make(r, t))
+
     def all_gather(self, parts, t, group=None):
         self.calls.append((t.device, t.dtype, tuple(t.shape)))
         assert len(parts) == self.world
@@ -37,6 +51,8 @@ def spy(monkeypatch):
         d = SpyDist(world, rank, make)
         monkeypatch.setattr(torch.distributed, "get_world_size", d.get_world_size)
         monkeypatch.setattr(torch.distributed, "all_gather", d.all_gather)
+        monkeypatch.setattr(torch.distributed, "get_rank", d.get_rank)
+        monkeypatch.setattr(torch.distributed, "gather", d.gather)
         return d
     return install
 
@@ -58,26 +74,37 @@ def test_gather_frames_device_tensors(spy, device):
     assert d.calls and all(c[0] == torch.device(device) and c[1] == torch.float64 for c in d.calls)
 
 
-def test_gather_landmark_rows_device_tensors(spy):
+@pytest.mark.parametrize("rank", [0, 2])
+@pytest.mark.parametrize("as_tensor", [False, True])
+def test_gather_rows_to_root_device_tensors(spy, rank, as_tensor):
     world = 3
-    rows = {r: (np.random.default_rng(r).normal(size=(5 + 3 * r, 3)).astype(np.float32),
-                np.random.default_rng(10 + r).random(5 + 3 * r) < 0.7) for r in range(world)}
+    rows = {r: np.random.default_rng(r).normal(size=(5 + 3 * r, 3)).astype(np.float32) for r in range(world)}
+    counts = [len(rows[r]) for r in range(world)]
+    m = max(counts)
 
     def make(r, t):
-        if t.dtype == torch.int64:                                  # the row counts
-            return torch.tensor([len(rows[r][1])], dtype=torch.int64, device=t.device)
-        out = torch.zeros_like(t)
-        X, k = rows[r]
-        out[: len(k), :3] = torch.from_numpy(X)
-        out[: len(k), 3] = torch.from_numpy(k.astype(np.float32))
+        out = torch.full_like(t, float("nan"))                      # padding must be dropped
+        out[: counts[r]] = torch.from_numpy(rows[r])
         return out
     dev = torch.device("cpu")
-    d = spy(world, 2, make)
-    X, keep = sharding.gather_landmark_rows(*rows[2], device=dev)
-    assert np.array_equal(X, np.concatenate([rows[r][0] for r in range(world)]))
-    assert np.array_equal(keep, np.concatenate([rows[r][1] for r in range(world)]))
-    assert [c[1] for c in d.calls] == [torch.int64, torch.float32]
-    assert all(c[0] == dev for c in d.calls)
+    d = spy(world, rank, make)
+    if as_tensor:                                                   # a device buffer of max(counts) rows
+        loc = torch.full((m, 3), float("nan"))
+        loc[: counts[rank]] = torch.from_numpy(rows[rank])
+    else:
+        loc = rows[rank]
+    got = sharding.gather_rows_to_root(loc, counts, device=dev)
+    if rank == 0:
+        assert got.dtype == np.float32 and np.array_equal(got, np.concatenate([rows[r] for r in range(world)]))
+    else:
+        assert got is None
+    assert d.calls == [(dev, torch.float32, (m, 3))]
+
+
+def test_rank_row_counts():
+    n = np.array([0, 3, 4, 0, 7, 1, 2])
+    assert sharding.rank_row_counts(n, 7, 3) == [7, 7, 3]       # blocks [0,3) [3,5) [5,7)
+    assert sharding.rank_row_counts(n, 7, 1) == [17]
 
 
 def test_gather_steps_frame_order(spy):

@@ -6,12 +6,17 @@ include/vo_spec.h / DESIGN.md §3: histograms summed in 2^-10 fixed point, vo_sp
 transcendentals (vs libm and OpenCV's fastAtan2), no removeDuplicatedSorted, and SSD
 computed as 2 - 2 cos from exact integer dot products.  oracle/liboracle_cv.so is the same
 C restatement built with -DVO_CV_LITERAL, which puts the literal float forms back.  These
-tests measure the divergence on the golden pair, a synthetic pair and a KITTI-00 stretch
-and enforce the thresholds DESIGN.md §3.8 states:
+tests measure the divergence on the golden pair, a synthetic pair, full-size KITTI-00 street
+frames and a KITTI-00 stretch, and enforce the thresholds DESIGN.md §3.8 states (round 5:
+tightened to the measured values plus a small margin, so that a perf-motivated change of
+vo_spec.h cannot give the margin back silently -- any such change must pass these BEFORE the
+goldens are regenerated):
 
-  keypoints   >= 99 % of keypoints agree (same x, y, octave, layer; angle within 2 deg)
-  descriptors mean L-inf <= 0.35, 99th percentile <= 2, max <= 24 (u8 units)
-  matches     Jaccard of the stereo match sets >= 0.98
+  keypoints   >= 99 % of keypoints agree (same x, y, octave, layer; angle within 2 deg), and
+              >= 99.8 % net of the exact duplicates the spec keeps and OpenCV's
+              removeDuplicatedSorted drops (measured 100 %: every other keypoint agrees)
+  descriptors mean L-inf <= 0.2, 99th percentile <= 1, max <= 4 (u8 units; measured 0.09-0.12 / 1 / 1)
+  matches     Jaccard of the stereo match sets >= 0.99 (measured 0.995-1.0)
   poses       8-frame trajectories differ by <= 3 % of the path (translation), <= 1 deg,
               and both stay within 3 % of the path of the rendered ground truth
 
@@ -22,26 +27,44 @@ import pytest
 from spec_divergence import pair_divergence, sequence_divergence
 
 
+AGREE, AGREE_DEDUP = 0.99, 0.998
+DESC_MEAN, DESC_P99, DESC_MAX = 0.2, 1, 4
+JACCARD = 0.99
+
+
 def _check_image(d):
-    assert d["agreement"] >= 0.99, d
-    assert d["desc_linf_mean"] <= 0.35 and d["desc_linf_p99"] <= 2 and d["desc_linf_max"] <= 24, d
+    assert d["agreement"] >= AGREE and d["agreement_dedup"] >= AGREE_DEDUP, d
+    assert d["desc_linf_mean"] <= DESC_MEAN and d["desc_linf_p99"] <= DESC_P99 and d["desc_linf_max"] <= DESC_MAX, d
+
+
+def _check_pair(d):
+    _check_image(d["left"])
+    _check_image(d["right"])
+    assert d["match_jaccard"] >= JACCARD, d
 
 
 def test_golden_pair_divergence(oracle):
     from pathlib import Path
     z = np.load(Path(__file__).parent / "golden" / "sift_pair.npz")
-    d = pair_divergence(oracle, z["left"], z["right"])
-    _check_image(d["left"])
-    _check_image(d["right"])
-    assert d["match_jaccard"] >= 0.98, d
+    _check_pair(pair_divergence(oracle, z["left"], z["right"]))
 
 
 def test_synthetic_pair_divergence(oracle, syn):
     L, R = syn.stereo_pair(syn.SEED_BASE + 41)
-    d = pair_divergence(oracle, L, R)
-    _check_image(d["left"])
-    _check_image(d["right"])
-    assert d["match_jaccard"] >= 0.98, d
+    _check_pair(pair_divergence(oracle, L, R))
+
+
+def test_kitti00_street_frames_divergence(oracle):
+    """Full-size (376 x 1241) frames rendered along KITTI-00's ground truth (keypoint
+    and descriptor agreement on the street world, where the full path runs)."""
+    import torch
+    from r7020e_visual_odometry_amd import street
+    torch.set_num_threads(4)
+    gt = street.kitti00_gt()
+    P0, P1 = street.kitti00_calib()
+    L, R = street.render_frames(street.kitti00_world(), gt, [700, 2600], P0, P1, chunk=2)
+    for i in range(2):
+        _check_pair(pair_divergence(oracle, L[i].numpy(), R[i].numpy()))
 
 
 def test_cv_literal_mode_is_a_different_implementation(oracle, syn):

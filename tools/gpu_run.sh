@@ -1,7 +1,7 @@
 #!/bin/bash
 # One evidence pass on a GPU box (run through gpurun from the repo root):
 #   bash tools/gpu_run.sh <outdir> [steps...]
-# steps (default: tests smoke bench): tests | smoke | bench | distbench | kprof | seqprof | pmc | insitu | attr | batch:<B> | probe:<tools binary>
+# steps (default: tests smoke bench): tests | smoke | bench | distbench | rehearse2 | py:<script>[:args] | kprof | seqprof | pmc | insitu | attr | batch:<B> | probe:<tools binary>
 #   | gpuonly:<pytest -k expr, + for spaces> | vtests:<variant>:<expr> | ab:<variant>[,<variant>...] (tools/variants/<name>/libvo.so)
 # Every GPU step has its own time limit and the chain stops at the first failure.
 set -e
@@ -45,6 +45,16 @@ for st in $STEPS; do
   probe:*)
     b=${st#probe:}; timeout -k 10 120 ./tools/$b > $O/$b.txt 2>&1 || { cat $O/$b.txt; exit 1; }
     cat $O/$b.txt ;;
+  py:*)
+    # py:<tools script>[:args, + for spaces] -- a short python tool on the GPU
+    a=${st#py:}; b=${a%%:*}; x=""; [ "$a" != "$b" ] && x=${a#*:}
+    timeout -k 10 300 python3 tools/$b ${x//+/ } > $O/${b%.py}.txt 2>&1 || { tail -20 $O/${b%.py}.txt; exit 1; }
+    tail -5 $O/${b%.py}.txt ;;
+  rehearse2)
+    # two ranks on this box's one GPU over gloo (the 8-GPU node runs nccl = RCCL): per-rank loop and tail
+    VO_BENCH_BACKEND=gloo VO_BENCH_SAME_GPU=1 timeout -k 10 600 python3 bench.py --gpus 2 --no-cpu --large-batch 0 > $O/rehearse2.json 2> $O/rehearse2.err \
+      || { tail -20 $O/rehearse2.err; exit 1; }
+    python3 -c "import json;d=json.loads([l for l in open('$O/rehearse2.json') if l.startswith('{')][0]);f=d['full_path'];print('rehearse2',d['n_gpus'],round(f['value']),f['landmark_rows'],f['accuracy']['ate_rmse_m'],f['per_rank_ms'])" ;;
   ab:*)
     v=${st#ab:}; timeout -k 10 900 bash tools/variant_bench.sh ${v//,/ } > $O/ab_${v//,/_}.txt 2>&1 || { cat $O/ab_${v//,/_}.txt; exit 1; }
     cat $O/ab_${v//,/_}.txt ;;
