@@ -478,6 +478,12 @@ __device__ __forceinline__ void blur_stream_body(const float* __restrict__ sp, i
     constexpr int F = (2 * RAD + P - 1) / P * P;           // ring-fill steps (no output)
     constexpr int E = F - 2 * RAD;                         // extra rows read above the band
     constexpr int RW = bs_rw(RAD, CPL);                    // staged row floats
+    // the staged form's LDS (stg) holds the source rows of at most kBaseMaxTH-row bands; the
+    // launcher caps TH, and a taller band (a probe or a future launcher) stores nothing rather
+    // than staging past stg into the other shared arrays (wave-uniform, before any LDS use)
+    if constexpr ((TAG & 4) != 0) {
+        if (TH > kBaseMaxTH) return;
+    }
     const int lane = threadIdx.x;
     const int xl = x0 - (XCH ? RH : 0) + CPL * lane;      // XCH: x0 is the first output column
     // halo lanes: [0, RH/CPL) left, [RH/CPL, 2*RH/CPL) right.  The others load lane 0's
@@ -2293,6 +2299,20 @@ void sift_enqueue_pyramid_tail(const Pyramid& py, SiftBuffers& b, int n_img, con
 {
     sift_enqueue_small(py, b, n_img, s, d_py);
     sift_enqueue_extrema(py, b, n_img, p, s, d_py, ext_o_begin, py.n_oct);
+}
+
+// k_orient sums each bin per histogram column in u32 fixed point (VO_ORIENT_COLS columns; one
+// weight < 361 * 2^10, |dI| <= 255), and a column receives 1/VO_ORIENT_COLS of the window's samples:
+// the window fits while (2r + 1)^2 <= VO_ORIENT_COLS * floor(2^32 / (361 * 2^10)).  r bounds the
+// orientation radius round(4.5 scl) for any refined scale (scl < sigma 2^((L + 0.5) / L), k_refine):
+// sigma up to ~17 at L = 1, ~21 at L = 3.
+bool sift_params_supported(const vo_sift_params& p)
+{
+    if (!(p.sigma > 0.0f) || !std::isfinite(p.sigma) || p.n_octave_layers < 1) return false;
+    const double scl = p.sigma * std::exp2((p.n_octave_layers + 0.5) / p.n_octave_layers);
+    const double r = std::ceil(VO_SIFT_ORI_RADIUS * scl) + 1;
+    const double per_column = std::floor(4294967296.0 / (361.0 * VO_DESC_FX_SCALE));
+    return (2 * r + 1) * (2 * r + 1) <= VO_ORIENT_COLS * per_column;
 }
 
 // Largest descriptor window radius any keypoint can have: k_refine accepts layer <= L with

@@ -244,7 +244,8 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
     if (ransac) c->rp = *ransac; else vo_default_ransac_params(&c->rp);
     if (calib) { c->calib = *calib; c->has_calib = true; }
     memcpy(c->pose, I4, sizeof(I4));
-    if (c->sp.n_octave_layers < 1 || c->sp.n_octave_layers > 5 || c->sp.max_keypoints < 16) {
+    if (c->sp.n_octave_layers < 1 || c->sp.n_octave_layers > 5 || c->sp.max_keypoints < 16 ||
+        !sift_params_supported(c->sp)) {
         fail(nullptr, VO_ERR_ARG, "vo_create: bad sift params");
         delete c;
         return nullptr;
@@ -585,12 +586,19 @@ int vo_match_f32(vo_ctx* c, const float* F1, int n1, int ld1, const float* F2, i
     // u8-valued rows (libvo / SIFT descriptors, what VO.m passes): the exact-integer spec of the
     // hot path; any other single features: the float SSD spec (match_f32_launch)
     if (!bad) return match_staged(c, n1, n2, pairs, capacity, n_pairs, "vo_match_f32");
-    if (!c->d_fa) {
+    if (!c->d_fa || !c->d_fbt || !c->d_fres) {
+        // all three or none: a failed allocation leaves the context without any of them, so the
+        // next call allocates again instead of launching on a null buffer
         const size_t fb = sizeof(float) * (size_t)c->sb.kp_cap * VO_DESC_LEN;
+        float* fa = nullptr; float* fbt = nullptr; int* fres = nullptr;
         hipError_t e;
-        if ((e = hipMalloc((void**)&c->d_fa, fb)) != hipSuccess || (e = hipMalloc((void**)&c->d_fbt, fb)) != hipSuccess ||
-            (e = hipMalloc((void**)&c->d_fres, sizeof(int) * c->sb.kp_cap)) != hipSuccess)
+        if ((e = hipMalloc((void**)&fa, fb)) != hipSuccess || (e = hipMalloc((void**)&fbt, fb)) != hipSuccess ||
+            (e = hipMalloc((void**)&fres, sizeof(int) * c->sb.kp_cap)) != hipSuccess) {
+            hipFree(fa); hipFree(fbt); hipFree(fres);
             return fail(c, VO_ERR_HIP, "vo_match_f32: %s", hipGetErrorString(e));
+        }
+        hipFree(c->d_fa); hipFree(c->d_fbt); hipFree(c->d_fres);
+        c->d_fa = fa; c->d_fbt = fbt; c->d_fres = fres;
     }
     match_f32_launch(c->d_ff[0], n1, ld1, c->d_ff[1], n2, ld2, col_major, c->d_fa, c->d_fbt, c->d_fres, c->mp, c->stream);
     std::vector<int> res((size_t)n1 + 1);

@@ -142,6 +142,9 @@ struct ImageSrc {
 };
 
 void build_pyramid_geometry(Pyramid& py, int rows, int cols, int n_img, const vo_sift_params& p);
+// Parameters the SIFT kernels' fixed-point and window bounds admit (vo_create refuses others):
+// sigma finite and > 0, and every orientation window small enough for k_orient's u32 column sums.
+bool sift_params_supported(const vo_sift_params& p);
 // View of images [img0, img0 + n) of b: every per-image array shifted (image-major layout).
 SiftBuffers sift_view(const SiftBuffers& b, const Pyramid& py, int img0, int n);
 hipError_t sift_alloc(SiftBuffers& b, const Pyramid& py, int kp_cap, int cand_cap);

@@ -185,3 +185,16 @@ def test_padded_and_flipped_views(vo, oracle, syn):
     k, d = ctx.sift(np.asfortranarray(L)[::-1])           # Fortran order, negative row stride
     assert np.array_equal(k, fk) and np.array_equal(d, fd)
     ctx.close()
+
+
+def test_create_refuses_sigma_beyond_the_orientation_bound(vo):
+    """ADVICE r4: k_orient's u32 column sums hold windows up to a bound (sift_params_supported);
+    vo_create refuses a Sigma whose orientation windows could exceed it instead of wrapping a bin."""
+    for sigma in (float("nan"), 0.0, -1.6, 40.0):
+        p = vo.default_sift_params()
+        p.sigma = sigma
+        with pytest.raises(vo.VOError):
+            vo.Context(64, 64, 1, sift=p)
+    p = vo.default_sift_params()
+    p.sigma = 4.0                                      # well inside the bound: accepted
+    vo.Context(64, 64, 1, sift=p).close()

@@ -166,7 +166,7 @@ int main()
                g / store_only(k_store_strip<20>, TH, 256) * 1e3, g / store_only(k_store_strip<24>, TH, 256) * 1e3,
                g / store_only(k_store_strip<31>, TH, 256) * 1e3);
     }
-    for (int TH : {32, 64, 128, 256}) {
+    for (int TH : {32, 64, 96}) {                          // the staged base takes bands of <= kBaseMaxTH (96) rows
         const float ms = store_only(k_store_strip<0>, TH, 256) / 100.0f;
         const float t0 = run<5>(u8, dst, plane, pitch, R, C, n, TH, K);
         const float t8 = run<5 | 8>(u8, dst, plane, pitch, R, C, n, TH, K);
@@ -188,9 +188,9 @@ int main()
             hipStream_t st;
             const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)((n_cu + 31) / 32), m);
             if (e != hipSuccess) { printf("%s 1/%d: %s\n", contig ? "contiguous" : "interleaved", div, hipGetErrorString(e)); continue; }
-            printf("%s CU mask 1/%d: VALU-bound %7.1f us | base %6.1f us (TH 128) | store-only %6.1f us\n",
+            printf("%s CU mask 1/%d: VALU-bound %7.1f us | base %6.1f us (TH 96) | store-only %6.1f us\n",
                    contig ? "contiguous" : "interleaved", div, run_valu(reinterpret_cast<float*>(u8), st),
-                   div <= 8 ? run<5>(u8, dst, plane, pitch, R, C, n, 128, K, st) : 0.0f, div <= 8 ? store_only_s(st) : 0.0f);
+                   div <= 8 ? run<5>(u8, dst, plane, pitch, R, C, n, 96, K, st) : 0.0f, div <= 8 ? store_only_s(st) : 0.0f);
         }
     return 0;
 }

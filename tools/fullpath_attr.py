@@ -7,7 +7,11 @@ then
       sequence leg, 2048 MSAC hypotheses) over the same frames;
   (c) per-kernel HIP-event times of (a) and (b) (profiling pass; collect syncs every stream),
       in ms per B frames;
-  (d) (a) on the bench's synthetic 1242x375 pairs, for the keypoint-density difference.
+  (d) (a) on the bench's synthetic 1242x375 pairs, for the keypoint-density difference;
+  (e) the "content" factor per kernel: isolated (synchronised) per-kernel times of (a) on the
+      street frames and on the synthetic pairs, with the keypoints' octave / layer mix and their
+      descriptor-window size (sum of squared octave-relative scales, which k_desc's and k_orient's
+      sample counts are proportional to) for one batch of each.
 usage: python tools/fullpath_attr.py [frames=1024] [batch=64]  -> one JSON line on stdout"""
 import json
 import sys
@@ -70,6 +74,35 @@ def profiled(fn):
     return {k: round(v[0] / nb, 4) for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])}
 
 
+def iso_times(c, dl, dr, nrep=3):
+    """(e): per-kernel times of synchronised calls (no overlap), ms per B frames."""
+    c.set_profiling(True)
+    for _ in range(nrep):
+        c.sift_match_batch_dev(dl, dr, B, stats=True)
+    torch.cuda.synchronize()
+    kt = c.kernel_times()
+    c.set_profiling(False)
+    return {k: round(v[0] / nrep, 4) for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])}
+
+
+def kp_mix(c, dl, dr):
+    """Octave / layer histogram and window-size sum of one batch's keypoints (all 2B images)."""
+    st = c.sift_match_batch_dev(dl, dr, B, stats=True)
+    octs, lays, w = [], [], 0.0
+    for i in range(2 * B):
+        k, _ = c.fetch_keypoints(i)
+        octs += k["octave"].tolist()
+        lays += k["layer"].tolist()
+        s = k["scale"].astype(np.float64) / np.exp2(k["octave"].astype(np.float64))   # octave-relative scale
+        w += float((s * s).sum())
+    octs, lays = np.array(octs), np.array(lays)
+    return {"keypoints_per_image": len(octs) / (2 * B), "stereo_matches_per_frame": float(np.mean([x[2] for x in st])),
+            "octave_hist": {int(o): int((octs == o).sum()) for o in np.unique(octs)},
+            "layer_hist": {int(l_): int((lays == l_).sum()) for l_ in np.unique(lays)},
+            "mean_octave_rel_scale": float(np.sqrt(w / max(len(octs), 1))),
+            "window_scl2_per_image": w / (2 * B)}
+
+
 t_sift = timed(sift_only)
 t_full = timed(full)
 outs = np.concatenate(full())
@@ -91,7 +124,13 @@ def syn_only():
 
 
 t_syn = timed(syn_only)
+iso_syn = iso_times(c2, sl.data_ptr(), sr.data_ptr())
+mix_syn = kp_mix(c2, sl.data_ptr(), sr.data_ptr())
 c2.close()
+c3 = vo.Context(street.KITTI_ROWS, street.KITTI_COLS, B)
+iso_street = iso_times(c3, dL.data_ptr(), dR.data_ptr())
+mix_street = kp_mix(c3, dL.data_ptr(), dR.data_ptr())
+c3.close()
 geom = {k: v for k, v in kt_full.items() if k not in kt_sift}
 shared = {k: round(kt_full[k] - kt_sift[k], 4) for k in kt_sift if k in kt_full}
 print(json.dumps({
@@ -104,6 +143,11 @@ print(json.dumps({
                             "synthetic": float(np.mean([s[0] + s[1] for s in st2]) / 2)},
     "mean_tracked": float(outs["n_tracked"][1:].mean()), "mean_inliers": float(outs["n_inliers"][1:].mean()),
     "kernel_ms_per_batch": {"sift_match": kt_sift, "full_path": kt_full},
+    "content": {"isolated_ms_per_batch": {"street": iso_street, "synthetic": iso_syn,
+                                          "street_minus_synthetic": {k: round(iso_street[k] - iso_syn.get(k, 0.0), 4)
+                                                                     for k in iso_street}},
+                "keypoints": {"street": mix_street, "synthetic": mix_syn},
+                "note": "street = the first B KITTI-00 frames at 376x1241, synthetic = the bench pairs at 375x1242"},
     "full_minus_sift": {"kernels_only_in_full_path": geom, "geometry_sum_ms": round(sum(geom.values()), 4),
                         "shared_kernels_delta_ms": shared},
 }))
