@@ -1436,6 +1436,9 @@ __device__ __forceinline__ void solve3_dev(const float H[9], const float b[3], f
 // of a wave work on different candidates (divergent iteration counts are fine).
 // Writes the refined fields of CandOut with npk = -1 (accepted, orientation
 // pending) or 0 (rejected).
+#ifndef VO_REFINE_BLOCKS
+#define VO_REFINE_BLOCKS 512      // grid-stride workgroups of 256 lanes (one lane per candidate)
+#endif
 __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                                 const uint32_t* __restrict__ cand, const int* __restrict__ n_cand,
                                                 CandOut* __restrict__ cout, int cand_cap, int n_img,
@@ -2333,7 +2336,7 @@ void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const v
     VO_LAUNCH(k_seg_count, gs, dim3(256), 0, s, b.mask, b.woff, py.n_words, py.n_seg);
     VO_LAUNCH(k_seg_scan, dim3(n_img), dim3(1024), 0, s, b.woff, b.n_cand, py.n_seg);
     VO_LAUNCH(k_seg_emit, gs, dim3(256), 0, s, d_py, b.mask, (const uint32_t*)b.woff, b.cand, b.cand_cap);
-    VO_LAUNCH(k_refine, dim3(512), dim3(256), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.cand_cap, n_img,
+    VO_LAUNCH(k_refine, dim3(VO_REFINE_BLOCKS), dim3(256), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.cand_cap, n_img,
               p.contrast_threshold, p.edge_threshold, p.sigma);
     const size_t fpre_bytes = sizeof(int) * (size_t)(n_img + 1);
     VO_LAUNCH_NAMED("k_orient", (k_orient<36>), dim3(kFeatureGrid), dim3(64), fpre_bytes, s, d_py, A, b.n_cand,

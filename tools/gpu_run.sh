@@ -55,6 +55,25 @@ for st in $STEPS; do
     VO_BENCH_BACKEND=gloo VO_BENCH_SAME_GPU=1 timeout -k 10 600 python3 bench.py --gpus 2 --no-cpu --large-batch 0 > $O/rehearse2.json 2> $O/rehearse2.err \
       || { tail -20 $O/rehearse2.err; exit 1; }
     python3 -c "import json;d=json.loads([l for l in open('$O/rehearse2.json') if l.startswith('{')][0]);f=d['full_path'];print('rehearse2',d['n_gpus'],round(f['value']),f['landmark_rows'],f['accuracy']['ate_rmse_m'],f['per_rank_ms'])" ;;
+  content_pmc)
+    # the same counters for the bench's synthetic pairs and for KITTI-00 street frames (content A/B)
+    for w in syn street; do
+      a=""; [ $w = street ] && a=street
+      timeout -s KILL 150 rocprofv3 --kernel-trace --output-format csv -d $O/cp_$w -o p --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES -- python3 tools/prof_run.py 64 2 $a > $O/cp_$w.log 2>&1 \
+        || { tail -20 $O/cp_$w.log; exit 1; }
+      python3 tools/pmc_sum.py $O/cp_$w > $O/cp_$w.txt
+      find $O/cp_$w -name "*.csv" -delete
+    done
+    grep -h "k_desc\|k_orient\|k_refine\|k_seg_emit" $O/cp_*.txt ;;
+  abfull:*)
+    # configs[1] and the full path (configs[2]) for the default library and each named variant
+    v=${st#abfull:}
+    for var in default ${v//,/ } default; do
+      if [ $var = default ]; then unset VO_LIBPATH; else export VO_LIBPATH=$GRAFT_REPO_ROOT/tools/variants/$var/libvo.so; fi
+      timeout -k 10 300 python3 bench.py --no-cpu --large-batch 0 > $O/abf_$var.json 2>/dev/null || { echo "$var failed"; exit 1; }
+      python3 -c "import json;d=json.load(open('$O/abf_$var.json'));f=d['full_path'];print('$var',round(d['value'],1),round(d['ms_per_step'],3),'full',round(f['value'],1),'refine',d['roofline']['kernel_ms_per_step'].get('k_refine'),f['kernel_ms_per_step'].get('k_refine'))"
+    done
+    unset VO_LIBPATH ;;
   ab:*)
     v=${st#ab:}; timeout -k 10 900 bash tools/variant_bench.sh ${v//,/ } > $O/ab_${v//,/_}.txt 2>&1 || { cat $O/ab_${v//,/_}.txt; exit 1; }
     cat $O/ab_${v//,/_}.txt ;;
