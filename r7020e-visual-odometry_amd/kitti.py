@@ -395,7 +395,7 @@ def assemble(steps: dict, X: np.ndarray, keep: np.ndarray, to_world=None):
 
 
 def finish_shard(ctx, outs, n: int, rank: int, world: int, device: int, group=None, distributed: bool = True,
-                 collective_device=None, timings: dict | None = None):
+                 collective_device=None, timings: dict | None = None, map_out=None):
     """The tail of a frame-sharded run after `run_shard(..., rows_to_host=False)` (SURVEY §8(e)
     step 4-5, `sharding.py`):
       1. one all-gather of the per-frame records (relative pose, status, counts: 23 doubles per
@@ -408,7 +408,9 @@ def finish_shard(ctx, outs, n: int, rank: int, world: int, device: int, group=No
     Returns (world poses [n, 4, 4], gathered per-frame records, landmarks float32 [L, 3] on rank 0
     -- single-rounded values, equal to a single-process run's rows -- and None on other ranks).
     `timings` (a dict) receives the seconds of each step: records, chain, world (device
-    transform), map (gather to rank 0 + its copy to the host)."""
+    transform), map (gather to rank 0 + its copy to the host).  `map_out`: rank 0's host buffer
+    for the map (CPU float32 tensor [>= rows, 3], e.g. pinned, allocated ahead; the returned map
+    is then a view of it)."""
     import time
     import torch
     from . import sharding, vo
@@ -429,10 +431,10 @@ def finish_shard(ctx, outs, n: int, rank: int, world: int, device: int, group=No
         raise RuntimeError(f"rank {rank}: {rows} landmark rows on the device, records say {counts[rank]}")
     t3 = time.perf_counter()
     if not distributed:
-        lm = buf[:rows].cpu().numpy()
+        lm = sharding.to_host(buf[:rows], map_out)
     else:
         lm = sharding.gather_rows_to_root(buf if collective_device is not None else buf[:rows].cpu(), counts,
-                                          group=group, device=collective_device)
+                                          group=group, device=collective_device, out=map_out)
     tm.update(records=t1 - t0, chain=t2 - t1, world=t3 - t2, map=time.perf_counter() - t3)
     return poses, steps, lm
 

@@ -122,12 +122,14 @@ def rank_row_counts(n_landmarks, n_frames: int, world: int) -> list[int]:
     return [int(n_landmarks[slice(*shard_range(n_frames, world, r))].sum()) for r in range(world)]
 
 
-def gather_rows_to_root(rows_local, counts, group=None, device=None):
+def gather_rows_to_root(rows_local, counts, group=None, device=None, out=None):
     """Rank 0 of the group receives every rank's world landmark rows (float32 [counts[r], 3], rank
     order = frame order) as one host array; the other ranks get None.  One dist.gather of
     buffers padded to max(counts): with device=<cuda device> the buffers stay on the device
     (RCCL over xGMI; `rows_local` may already be such a tensor of at least max(counts) rows), with
-    device=None they are CPU tensors (gloo).  Only rank 0 copies rows to the host."""
+    device=None they are CPU tensors (gloo).  Only rank 0 copies rows to the host: into `out` (a
+    CPU float32 tensor [>= sum(counts), 3], e.g. pinned memory allocated ahead) when given, the
+    result then being a view of it."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
@@ -150,7 +152,18 @@ def gather_rows_to_root(rows_local, counts, group=None, device=None):
         return None
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.gather(buf, parts, dst=dst, group=group)
-    return torch.cat([p[:c] for p, c in zip(parts, counts)]).cpu().numpy()
+    return to_host(torch.cat([p[:c] for p, c in zip(parts, counts)]), out)
+
+
+def to_host(rows, out=None):
+    """float32 [n, 3] rows -> host numpy: a copy into `out` (CPU tensor with room for them, e.g.
+    pinned memory allocated before a timed region: one DMA, no page-locking on the way) viewed as
+    numpy, else a plain .cpu() copy."""
+    n = rows.shape[0]
+    if out is not None and out.dim() == 2 and out.shape[0] >= n and out.shape[1] == 3 and out.dtype == rows.dtype:
+        out[:n].copy_(rows)
+        return out[:n].numpy()
+    return rows.cpu().numpy()
 
 
 def world_landmarks(poses: np.ndarray, n_landmarks: np.ndarray, X: np.ndarray, keep: np.ndarray,

@@ -76,7 +76,8 @@ def test_gather_frames_device_tensors(spy, device):
 
 @pytest.mark.parametrize("rank", [0, 2])
 @pytest.mark.parametrize("as_tensor", [False, True])
-def test_gather_rows_to_root_device_tensors(spy, rank, as_tensor):
+@pytest.mark.parametrize("with_out", [False, True])
+def test_gather_rows_to_root_device_tensors(spy, rank, as_tensor, with_out):
     world = 3
     rows = {r: np.random.default_rng(r).normal(size=(5 + 3 * r, 3)).astype(np.float32) for r in range(world)}
     counts = [len(rows[r]) for r in range(world)]
@@ -93,9 +94,12 @@ def test_gather_rows_to_root_device_tensors(spy, rank, as_tensor):
         loc[: counts[rank]] = torch.from_numpy(rows[rank])
     else:
         loc = rows[rank]
-    got = sharding.gather_rows_to_root(loc, counts, device=dev)
+    out = torch.full((sum(counts) + 3, 3), -7.0) if with_out else None        # a host buffer allocated ahead
+    got = sharding.gather_rows_to_root(loc, counts, device=dev, out=out)
     if rank == 0:
         assert got.dtype == np.float32 and np.array_equal(got, np.concatenate([rows[r] for r in range(world)]))
+        if with_out:                                                # a view of the caller's buffer
+            assert np.shares_memory(got, out.numpy()) and (out[sum(counts):] == -7.0).all()
     else:
         assert got is None
     assert d.calls == [(dev, torch.float32, (m, 3))]
