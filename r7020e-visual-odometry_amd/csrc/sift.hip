@@ -1583,7 +1583,11 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
 #pragma unroll
         for (int b2 = 4 * lane; b2 < HS * NC; b2 += 256) *reinterpret_cast<u4_t*>(&hp[b2]) = u4_t{0u, 0u, 0u, 0u};
         __syncthreads();
+#if defined(VO_ORIENT_DIAG)
+        const int side = 2 * radius + 1, nsamp = 0;  // diagnostic build (timing only): no sample loop
+#else
         const int side = 2 * radius + 1, nsamp = side * side;
+#endif
         const float inv_side = 1.0f / (float)side;          // (s + 0.5) * inv_side is exact enough to floor (s < 2^22)
         // gradient loads through a buffer resource based at gim - P - 1: one 32-bit lane offset
         // (the window row as a 24-bit multiply of the clamped row step), row y as one 12-B load
@@ -1801,6 +1805,9 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
         const float exp_scale = -1.0f / ((float)(DW * DW) * 0.5f);
         const float hist_width = VO_SIFT_DESCR_SCL * q.scl;
         int radius = vo_round(hist_width * 1.4142135623730951f * (float)(DW + 1) * 0.5f);
+#if defined(VO_DESC_DIAG) && VO_DESC_DIAG >= 2
+        radius = 0;                                  // diagnostic build (timing only): no window tables
+#endif
         if (radius > g.dmax) radius = g.dmax;
         if (radius > VO_SIFT_DESCR_RMAX) radius = VO_SIFT_DESCR_RMAX;
         radius = min(radius, rcap);                 // (never binds: rcap bounds every refined scale)
@@ -1877,7 +1884,11 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
             if (lane < 8) rtab[nrows + 1 + lane] = 0xFFFFu;
         }
         __syncthreads();
+#if defined(VO_DESC_DIAG) && VO_DESC_DIAG >= 1
+        const int nsamp = 0;                         // diagnostic build (timing only): no sample loop
+#else
         const int nsamp = (int)rtab[nrows];
+#endif
         uint32_t* hc = hfx + (lane & (DCOPIES - 1)) * DCS;
         // one sample: weights, bins, fixed-point LDS atomics
         auto accum = [&](float c_rot, float r_rot, float w, float dx, float dy) {
