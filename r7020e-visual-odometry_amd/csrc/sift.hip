@@ -33,6 +33,8 @@ struct Kern { float k[VO_SIFT_MAX_RADIUS + 1]; int r; float* nb; int nb_pitch, n
 
 // ---------------------------------------------------------------------------
 // geometry (host)
+static int desc_radius_cap(const Pyramid& py, const vo_sift_params& p);
+
 // ---------------------------------------------------------------------------
 void build_pyramid_geometry(Pyramid& py, int rows, int cols, int n_img, const vo_sift_params& p)
 {
@@ -79,6 +81,7 @@ void build_pyramid_geometry(Pyramid& py, int rows, int cols, int n_img, const vo
     py.ebase[py.n_oct] = t;
     py.n_units = t;
     py.n_seg = (w + VO_SEG_WORDS - 1) / VO_SEG_WORDS;
+    py.dcap = desc_radius_cap(py, p);
 }
 
 SiftBuffers sift_view(const SiftBuffers& b, const Pyramid& py, int img0, int n)
@@ -90,6 +93,8 @@ SiftBuffers sift_view(const SiftBuffers& b, const Pyramid& py, int img0, int n)
     v.woff = b.woff + (size_t)img0 * py.n_seg;
     v.cand = b.cand + (size_t)img0 * b.cand_cap;
     v.n_cand = b.n_cand + img0;
+    v.acc = b.acc + (size_t)img0 * b.cand_cap;
+    v.n_acc = b.n_acc + img0;
     v.cout = b.cout + (size_t)img0 * b.cand_cap;
     v.koff = b.koff + (size_t)img0 * b.cand_cap;
     v.n_kp = b.n_kp + img0;
@@ -113,6 +118,8 @@ hipError_t sift_alloc(SiftBuffers& b, const Pyramid& py, int kp_cap, int cand_ca
     VO_ALLOC(b.woff, sizeof(uint32_t) * (size_t)py.n_seg * n + 8);
     VO_ALLOC(b.cand, sizeof(uint32_t) * (size_t)cand_cap * n);
     VO_ALLOC(b.n_cand, sizeof(int) * n);
+    VO_ALLOC(b.acc, sizeof(int) * (size_t)cand_cap * n);
+    VO_ALLOC(b.n_acc, sizeof(int) * n);
     VO_ALLOC(b.cout, sizeof(CandOut) * (size_t)cand_cap * n);
     VO_ALLOC(b.koff, sizeof(uint32_t) * (size_t)cand_cap * n);
     VO_ALLOC(b.n_kp, sizeof(int) * n);
@@ -126,7 +133,7 @@ hipError_t sift_alloc(SiftBuffers& b, const Pyramid& py, int kp_cap, int cand_ca
 
 void sift_free(SiftBuffers& b)
 {
-    hipFree(b.arena); hipFree(b.tmp); hipFree(b.mask); hipFree(b.woff); hipFree(b.cand); hipFree(b.n_cand);
+    hipFree(b.arena); hipFree(b.tmp); hipFree(b.mask); hipFree(b.woff); hipFree(b.cand); hipFree(b.n_cand); hipFree(b.acc); hipFree(b.n_acc);
     hipFree(b.cout); hipFree(b.koff); hipFree(b.n_kp); hipFree(b.kp); hipFree(b.kpi); hipFree(b.desc); hipFree(b.meta);
     b = SiftBuffers();
 }
@@ -1216,8 +1223,10 @@ __global__ __launch_bounds__(256) void k_seg_count(const unsigned long long* __r
     if (tid == 0) segc[(size_t)img * nseg + seg] = red[0] + red[1] + red[2] + red[3];
 }
 
-__global__ __launch_bounds__(1024) void k_seg_scan(uint32_t* __restrict__ segc, int* __restrict__ n_cand, int nseg)
+__global__ __launch_bounds__(1024) void k_seg_scan(uint32_t* __restrict__ segc, int* __restrict__ n_cand, int* __restrict__ n_acc,
+                                                   int nseg)
 {
+    if (threadIdx.x == 0) n_acc[blockIdx.x] = 0;           // k_refine appends this image's accepted candidates
     __shared__ uint32_t sh[32];
     const int img = blockIdx.x, tid = threadIdx.x;
     uint32_t v = tid < nseg ? segc[(size_t)img * nseg + tid] : 0u;
@@ -1441,8 +1450,8 @@ __device__ __forceinline__ void solve3_dev(const float H[9], const float b[3], f
 #endif
 __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                                 const uint32_t* __restrict__ cand, const int* __restrict__ n_cand,
-                                                CandOut* __restrict__ cout, int cand_cap, int n_img,
-                                                float contrast_thr, float edge_thr, float sigma)
+                                                CandOut* __restrict__ cout, int* __restrict__ acc, int* __restrict__ n_acc,
+                                                int cand_cap, int n_img, float contrast_thr, float edge_thr, float sigma)
 {
     const int L = py->L;
     __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
@@ -1517,6 +1526,24 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
         out->xo = xo; out->yo = yo; out->scl = scl; out->response = resp;
         out->o = o; out->layer = layer; out->r = r; out->c = c;
         out->npk = ok ? -1 : 0;
+        // the accepted candidates as a list (k_orient walks only those: on KITTI-00 street frames
+        // ~6 in 7 candidates are rejected here, profiles/r05_d_content_pmc_*); the list order is
+        // free -- every result is stored at its candidate's index
+#if VO_ACC_LIST
+        // one atomic per (wave, image): the lanes of a wave hold consecutive candidates, one image
+        // (two at an image boundary); per-lane atomics on 128 counters serialised k_refine 7x
+        unsigned long long todo = __ballot(ok);
+        while (todo) {
+            const int leader = __builtin_ctzll(todo);
+            const int limg = __shfl(img, leader);
+            const unsigned long long m = __ballot(ok && img == limg);
+            int base = 0;
+            if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(n_acc + limg, __popcll(m));
+            base = __shfl(base, leader);
+            if (ok && img == limg) acc[(size_t)limg * cand_cap + base + __popcll(m & ((1ull << (threadIdx.x & 63)) - 1ull))] = kidx;
+            todo &= ~m;
+        }
+#endif
 #undef DOGV
     }
 }
@@ -1552,8 +1579,8 @@ __device__ __forceinline__ uint32_t desc_fxq(float v)
 #endif
 template <int HS>
 __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* __restrict__ py, const float* __restrict__ arena,
-                                               const int* __restrict__ n_cand, CandOut* __restrict__ cout,
-                                               int cand_cap, int n_img)
+                                               const int* __restrict__ n_acc, const int* __restrict__ acc,
+                                               CandOut* __restrict__ cout, int cand_cap, int n_img)
 {
     // HS: bins per lane column (>= 36).  Layout hp[bin * 64 + lane].
     constexpr int NC = VO_ORIENT_COLS;             // histogram columns: lane l adds into column l % NC
@@ -1563,12 +1590,17 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
     __shared__ float hs[VO_SIFT_ORI_BINS];
     const int lane = threadIdx.x;
     extern __shared__ int fpre[];                    // n_img + 1 ints (dynamic: sized by the launch)
-    const long total = flat_setup(n_cand, cand_cap, n_img, fpre);
+    const long total = flat_setup(n_acc, cand_cap, n_img, fpre);
     for (long t = blockIdx.x; t < total; t += gridDim.x) {
-        int img, kidx;
-        flat_find_wave(fpre, n_img, t, img, kidx);
+        int img, a;
+        flat_find_wave(fpre, n_img, t, img, a);
+#if VO_ACC_LIST
+        const int kidx = __builtin_amdgcn_readfirstlane(acc[(size_t)img * cand_cap + a]);
+#else
+        const int kidx = a;                              // every candidate (n_acc = n_cand)
+#endif
         CandOut* out = cout + (size_t)img * cand_cap + kidx;
-        if (__builtin_amdgcn_readfirstlane(out->npk) != -1) continue;
+        if (!VO_ACC_LIST && __builtin_amdgcn_readfirstlane(out->npk) != -1) continue;
         const int o = __builtin_amdgcn_readfirstlane(out->o), layer = __builtin_amdgcn_readfirstlane(out->layer);
         const int r = __builtin_amdgcn_readfirstlane(out->r), c = __builtin_amdgcn_readfirstlane(out->c);
         const float scl = out->scl;
@@ -1693,15 +1725,18 @@ __global__ __launch_bounds__(1024) void k_scan_cands(const CandOut* __restrict__
     if (tid == 0) n_kp[img] = (int)total;
 }
 
-__global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict__ n_cand, const uint32_t* __restrict__ koff,
-                         vo_keypoint* __restrict__ kp, KpInt* __restrict__ kpi, int cand_cap, int kp_cap, int n_img,
-                         int upsample)
+// one thread per accepted candidate (k_refine's list; each writes its own keypoint slots, so the
+// list order does not matter)
+__global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict__ n_acc, const int* __restrict__ acc,
+                         const uint32_t* __restrict__ koff, vo_keypoint* __restrict__ kp, KpInt* __restrict__ kpi,
+                         int cand_cap, int kp_cap, int n_img, int upsample)
 {
     __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
-    const long total = flat_setup(n_cand, cand_cap, n_img, fpre);
+    const long total = flat_setup(n_acc, cand_cap, n_img, fpre);
     for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-        int img, k;
-        flat_find(fpre, n_img, t, img, k);
+        int img, a;
+        flat_find(fpre, n_img, t, img, a);
+        const int k = VO_ACC_LIST ? acc[(size_t)img * cand_cap + a] : a;
         const CandOut& co = cout[(size_t)img * cand_cap + k];
         const int npk = co.npk;
         if (!npk) continue;
@@ -1756,138 +1791,179 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
 #ifndef VO_DESC_U
 #define VO_DESC_U 2               // blocks of 64 samples per batch
 #endif
+// The keypoint's descriptor window tables into LDS (hdr, rtab, wtab; layout of dt_stride): its rotation,
+// radius, sample count, row table -- each window row i's column interval [jlo, jhi] inside the
+// rotated 4x4-cell square and the image interior, flattened by a prefix sum -- and the separable
+// window weights.  Ends with the tables visible to the whole wave.
+// One packed row entry per window row r: (index of the row's first sample) | (its first column j,
+// int16) << 16; entry nrows is the sample count, entries nrows+1 .. nrows+8 a 0xFFFF sentinel
+// start.  Starts fit 16 bits: a window never holds more than its (2 r + 1)^2 square, which
+// the cap r <= VO_SIFT_DESCR_RMAX = 127 bounds by 65025 (the rotated square alone is
+// ~2 r^2 + O(r) samples, but a capped radius can leave the whole square inside it).
+static_assert((2 * VO_SIFT_DESCR_RMAX + 1) * (2 * VO_SIFT_DESCR_RMAX + 1) <= 0xFFFF, "16-bit row starts");
+__device__ __forceinline__ void desc_tables(const Pyramid* __restrict__ py, KpInt q, int dcap, uint32_t* hdr, uint32_t* rtab,
+                                            float* wtab, int lane)
+{
+    q.o = __builtin_amdgcn_readfirstlane(q.o);
+    q.layer = __builtin_amdgcn_readfirstlane(q.layer);
+    const OctGeom& g = py->oct[q.o];
+    const int rows = g.rows, cols = g.cols;
+    float ori = 360.0f - q.angle;
+    if (fabsf(ori - 360.0f) < VO_FLT_EPSILON) ori = 0.0f;
+    const int px = vo_round(q.xo), pyy = vo_round(q.yo);
+    float sin_t, cos_t;
+    vo_sincos_deg(ori, &sin_t, &cos_t);
+    const float exp_scale = -1.0f / ((float)(DW * DW) * 0.5f);
+    const float hist_width = VO_SIFT_DESCR_SCL * q.scl;
+    int radius = vo_round(hist_width * 1.4142135623730951f * (float)(DW + 1) * 0.5f);
+#if defined(VO_DESC_DIAG) && VO_DESC_DIAG >= 2
+    radius = 0;                                  // diagnostic build (timing only): no window tables
+#endif
+    if (radius > g.dmax) radius = g.dmax;
+    if (radius > VO_SIFT_DESCR_RMAX) radius = VO_SIFT_DESCR_RMAX;
+    radius = min(radius, dcap);                 // (never binds: dcap bounds every refined scale)
+    cos_t = cos_t / hist_width;
+    sin_t = sin_t / hist_width;
+    {
+        const float wsc = exp_scale / (hist_width * hist_width);
+        // x 32 per factor: the product carries the fixed-point pre-scale 2^10 (exact, powers of two)
+        for (int k2 = lane; k2 <= radius; k2 += 64) wtab[k2] = vo_sift_wt(wsc, k2) * 32.0f;
+    }
+    // Only ~half of the (2r+1)^2 window lies inside the rotated 4x4-cell square.  Each
+    // window row i gets a conservative column interval [jlo, jhi] (a superset: +-2
+    // columns of margin over the real-arithmetic bounds, clamped to the image
+    // interior); rows are flattened with a prefix sum, and the exact float test below
+    // still decides every sample, so the histogram is unchanged (fixed-point sums are
+    // order-free) while the wave no longer idles through rejected samples.
+    const int nrows = 2 * radius + 1;
+    const float inv_ct = fabsf(cos_t) > 1e-9f ? 1.0f / cos_t : 0.0f, inv_st = fabsf(sin_t) > 1e-9f ? 1.0f / sin_t : 0.0f;
+    for (int rr = lane; rr < nrows; rr += 64) {
+        const int i = rr - radius, r = pyy + i;
+        int jlo = -radius, jhi = radius;
+        if (r <= 0 || r >= rows - 1) { jlo = 1; jhi = 0; }
+        else {
+            // |j*ct - i*st| < lim  and  |j*st + i*ct| < lim  (rbin = r_rot + 1.5 in (-1, DW)); lim is
+            // 1e-3 bin widths wider than the test below, far above the float error of the test
+            // (~1e-6) and of these bounds (< 1e-4 columns at r <= RMAX), so [floor(a), ceil(b)]
+            // holds every accepted column
+            const float fi = (float)i, lim = 0.5f * DW + 0.5f + 1e-3f, cap = (float)(radius + 2);
+            if (fabsf(cos_t) > 1e-9f) {
+                float a = (fi * sin_t - lim) * inv_ct, b = (fi * sin_t + lim) * inv_ct;
+                if (a > b) { const float t2 = a; a = b; b = t2; }
+                a = fminf(fmaxf(a, -cap), cap); b = fminf(fmaxf(b, -cap), cap);
+                jlo = max(jlo, (int)floorf(a)); jhi = min(jhi, (int)ceilf(b));
+            } else if (fabsf(fi * sin_t) >= lim) { jlo = 1; jhi = 0; }
+            if (fabsf(sin_t) > 1e-9f) {
+                float a = (-fi * cos_t - lim) * inv_st, b = (-fi * cos_t + lim) * inv_st;
+                if (a > b) { const float t2 = a; a = b; b = t2; }
+                a = fminf(fmaxf(a, -cap), cap); b = fminf(fmaxf(b, -cap), cap);
+                jlo = max(jlo, (int)floorf(a)); jhi = min(jhi, (int)ceilf(b));
+            } else if (fabsf(fi * cos_t) >= lim) { jlo = 1; jhi = 0; }
+            jlo = max(jlo, 1 - px); jhi = min(jhi, cols - 2 - px);
+            // trim the superset to the exact set: the float test in k_desc is monotone
+            // in j on each side (rotations of a row are monotone float sequences),
+            // so the accepted columns form one interval inside [jlo, jhi]
+            const float fi_s = (float)i * sin_t, fi_c = (float)i * cos_t;
+            auto inside = [&](int j) {
+                const float cr = (float)j * cos_t - fi_s, rr2 = (float)j * sin_t + fi_c;
+                const float rb = rr2 + (float)(DW / 2) - 0.5f, cb = cr + (float)(DW / 2) - 0.5f;
+                return rb > -1.0f && rb < (float)DW && cb > -1.0f && cb < (float)DW;
+            };
+            while (jlo <= jhi && !inside(jlo)) ++jlo;
+            while (jhi >= jlo && !inside(jhi)) --jhi;
+        }
+        // row length for now (prefixed below), first column in the high half
+        rtab[rr] = (uint32_t)(jhi >= jlo ? jhi - jlo + 1 : 0) | ((uint32_t)(uint16_t)(int16_t)jlo << 16);
+    }
+    __syncthreads();
+    {   // wave-parallel exclusive prefix over the rows (<= 2*RMAX+1): lane owns a chunk of rows
+        constexpr int PER_MAX = (2 * VO_SIFT_DESCR_RMAX + 1 + 63) / 64;
+        const int per = (nrows + 63) >> 6, r0w = lane * per;
+        uint32_t ent[PER_MAX];
+        int sum = 0;
+#pragma unroll
+        for (int q2 = 0; q2 < PER_MAX; ++q2) {
+            ent[q2] = (q2 < per && r0w + q2 < nrows) ? rtab[r0w + q2] : 0u;
+            sum += (int)(ent[q2] & 0xFFFFu);
+        }
+        const int inc = wave_incl_scan(sum);
+        int acc = inc - sum;
+#pragma unroll
+        for (int q2 = 0; q2 < PER_MAX; ++q2)
+            if (q2 < per && r0w + q2 < nrows) { rtab[r0w + q2] = (uint32_t)acc | (ent[q2] & 0xFFFF0000u); acc += (int)(ent[q2] & 0xFFFFu); }
+        if (lane == 63) { rtab[nrows] = (uint32_t)inc; hdr[DT_NSAMP] = (uint32_t)inc; }
+        if (lane < 8) rtab[nrows + 1 + lane] = 0xFFFFu;
+        if (lane == 0) {
+            hdr[DT_ORI] = __float_as_uint(ori); hdr[DT_PX] = (uint32_t)px; hdr[DT_PY] = (uint32_t)pyy;
+            hdr[DT_RADIUS] = (uint32_t)radius; hdr[DT_COS] = __float_as_uint(cos_t); hdr[DT_SIN] = __float_as_uint(sin_t);
+            hdr[DT_NROWS] = (uint32_t)nrows; hdr[DT_O] = (uint32_t)q.o; hdr[DT_LAYER] = (uint32_t)q.layer;
+        }
+    }
+    __syncthreads();
+}
+
 template <int DCOPIES>
 __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                              const KpInt* __restrict__ kpi, const int* __restrict__ n_kp,
-                                             uint8_t* __restrict__ desc, DescMeta* __restrict__ meta, int kp_cap, int n_img,
-                                             int rcap)
+                                             uint8_t* __restrict__ desc,
+                                             DescMeta* __restrict__ meta, int kp_cap, int n_img)
 {
     static_assert(DCS >= DHIST, "copy stride holds a histogram");
     __shared__ __attribute__((aligned(16))) uint32_t hfx[DCOPIES * DCS];
-    // One packed entry per window row r: (index of the row's first sample) | (its first column j,
-    // int16) << 16; entry nrows is the sample count, entries nrows+1 .. nrows+8 a 0xFFFF sentinel
-    // start.  Starts fit 16 bits: a window never holds more than its (2 r + 1)^2 square, which
-    // the cap r <= VO_SIFT_DESCR_RMAX = 127 bounds by 65025 (the rotated square alone is
-    // ~2 r^2 + O(r) samples, but a capped radius can leave the whole square inside it).
-    // 6.3 KB of LDS with the histograms, tables and prefix at batch 64 -> 5 one-wave workgroups
-    // per SIMD with room to spare for the blur waves beside them.
-    static_assert((2 * VO_SIFT_DESCR_RMAX + 1) * (2 * VO_SIFT_DESCR_RMAX + 1) <= 0xFFFF, "16-bit row starts");
-    // Dynamic LDS, sized by the launch for this pyramid (desc_lds_bytes): the row table (2 rcap + 10
-    // entries), the separable window weights wtab[0 .. rcap] (vo_spec.h vo_sift_wt: w(i, j) =
-    // wtab[|i|] * wtab[|j|]) and the image prefix (n_img + 1).  rcap bounds every keypoint's radius
-    // (the largest refined scale the parameters allow, capped at VO_SIFT_DESCR_RMAX): 1.1 KB instead
-    // of 2.6 KB at the default parameters, so the descriptor's one-wave workgroups leave LDS for the
-    // scale-space waves that share their CUs.
+    // Dynamic LDS, sized by the launch for this pyramid: the keypoint's window tables (desc_tables,
+    // dt_stride(dcap) words: header, row table, separable window weights wtab[0 .. radius] --
+    // vo_spec.h vo_sift_wt: w(i, j) = wtab[|i|] * wtab[|j|]) and the image prefix (n_img + 1).
+    // (The tables as a separate full-occupancy launch, k_desc_prep, measured slower: 0.35 ms for
+    // that launch against 0.23 ms they cost inside k_desc, profiles/r05_g_*.)  dcap bounds every keypoint's radius (the largest refined scale the parameters
+    // allow, capped at VO_SIFT_DESCR_RMAX): ~0.6 KB at the default parameters, so the descriptor's
+    // one-wave workgroups leave LDS for the scale-space waves that share their CUs.
     extern __shared__ uint32_t dyn[];
-    uint32_t* const rtab = dyn;
-    float* const wtab = reinterpret_cast<float*>(dyn + 2 * rcap + 10);
-    int* const fpre = reinterpret_cast<int*>(dyn + 3 * rcap + 11);
+    const int dcap = py->dcap, ts = dt_stride(dcap);
+    const uint32_t* const hdr = dyn;
+    const uint32_t* const rtab = dyn + dt_rtab_off();
+    const float* const wtab = reinterpret_cast<const float*>(dyn + dt_wtab_off(dcap));
+    int* const fpre = reinterpret_cast<int*>(dyn + ts);
     const int lane = threadIdx.x;
     const long total = flat_setup(n_kp, kp_cap, n_img, fpre);
+    const float bins_per_deg = (float)DN / 360.0f;
+#if VO_FEAT_PREFETCH
+    // the next keypoint's record is loaded one iteration ahead, so its latency overlaps this
+    // keypoint's work instead of heading the next one's table build
+    int img_n = 0, k_n = 0;
+    KpInt q_n{};
+    if (blockIdx.x < total) {
+        flat_find_wave(fpre, n_img, blockIdx.x, img_n, k_n);
+        q_n = kpi[(size_t)img_n * kp_cap + k_n];
+    }
+#endif
     for (long t = blockIdx.x; t < total; t += gridDim.x) {
         int img, k;
+#if VO_FEAT_PREFETCH
+        img = img_n; k = k_n;
+        const KpInt q = q_n;
+        if (t + gridDim.x < total) {
+            flat_find_wave(fpre, n_img, t + gridDim.x, img_n, k_n);
+            q_n = kpi[(size_t)img_n * kp_cap + k_n];
+        }
+#else
         flat_find_wave(fpre, n_img, t, img, k);
-        KpInt q = kpi[(size_t)img * kp_cap + k];
-        q.o = __builtin_amdgcn_readfirstlane(q.o);              // wave-uniform -> scalar geometry loads
-        q.layer = __builtin_amdgcn_readfirstlane(q.layer);
-        const OctGeom& g = py->oct[q.o];
-        const int rows = g.rows, cols = g.cols, P = g.pitch;
-        const float* gim = arena + g.g_off[q.layer] + img * py->istride;
+        const KpInt q = kpi[(size_t)img * kp_cap + k];
+#endif
         static_assert((DCOPIES * DCS) % 4 == 0, "16-B zeroing");
         typedef uint32_t u4z_t __attribute__((ext_vector_type(4)));
         for (int b = 4 * lane; b < DCOPIES * DCS; b += 256) *reinterpret_cast<u4z_t*>(&hfx[b]) = u4z_t{0u, 0u, 0u, 0u};
-        float ori = 360.0f - q.angle;
-        if (fabsf(ori - 360.0f) < VO_FLT_EPSILON) ori = 0.0f;
-        const int px = vo_round(q.xo), pyy = vo_round(q.yo);
-        float sin_t, cos_t;
-        vo_sincos_deg(ori, &sin_t, &cos_t);
-        const float bins_per_deg = (float)DN / 360.0f;
-        const float exp_scale = -1.0f / ((float)(DW * DW) * 0.5f);
-        const float hist_width = VO_SIFT_DESCR_SCL * q.scl;
-        int radius = vo_round(hist_width * 1.4142135623730951f * (float)(DW + 1) * 0.5f);
-#if defined(VO_DESC_DIAG) && VO_DESC_DIAG >= 2
-        radius = 0;                                  // diagnostic build (timing only): no window tables
-#endif
-        if (radius > g.dmax) radius = g.dmax;
-        if (radius > VO_SIFT_DESCR_RMAX) radius = VO_SIFT_DESCR_RMAX;
-        radius = min(radius, rcap);                 // (never binds: rcap bounds every refined scale)
-        cos_t = cos_t / hist_width;
-        sin_t = sin_t / hist_width;
-        {
-            const float wsc = exp_scale / (hist_width * hist_width);
-            // x 32 per factor: the product carries the fixed-point pre-scale 2^10 (exact, powers of two)
-            for (int k2 = lane; k2 <= radius; k2 += 64) wtab[k2] = vo_sift_wt(wsc, k2) * 32.0f;
-        }
-        // Only ~half of the (2r+1)^2 window lies inside the rotated 4x4-cell square.  Each
-        // window row i gets a conservative column interval [jlo, jhi] (a superset: +-2
-        // columns of margin over the real-arithmetic bounds, clamped to the image
-        // interior); rows are flattened with a prefix sum, and the exact float test below
-        // still decides every sample, so the histogram is unchanged (fixed-point sums are
-        // order-free) while the wave no longer idles through rejected samples.
-        const int nrows = 2 * radius + 1;
-        const float inv_ct = fabsf(cos_t) > 1e-9f ? 1.0f / cos_t : 0.0f, inv_st = fabsf(sin_t) > 1e-9f ? 1.0f / sin_t : 0.0f;
-        for (int rr = lane; rr < nrows; rr += 64) {
-            const int i = rr - radius, r = pyy + i;
-            int jlo = -radius, jhi = radius;
-            if (r <= 0 || r >= rows - 1) { jlo = 1; jhi = 0; }
-            else {
-                // |j*ct - i*st| < lim  and  |j*st + i*ct| < lim  (rbin = r_rot + 1.5 in (-1, DW)); lim is
-                // 1e-3 bin widths wider than the test below, far above the float error of the test
-                // (~1e-6) and of these bounds (< 1e-4 columns at r <= RMAX), so [floor(a), ceil(b)]
-                // holds every accepted column
-                const float fi = (float)i, lim = 0.5f * DW + 0.5f + 1e-3f, cap = (float)(radius + 2);
-                if (fabsf(cos_t) > 1e-9f) {
-                    float a = (fi * sin_t - lim) * inv_ct, b = (fi * sin_t + lim) * inv_ct;
-                    if (a > b) { const float t2 = a; a = b; b = t2; }
-                    a = fminf(fmaxf(a, -cap), cap); b = fminf(fmaxf(b, -cap), cap);
-                    jlo = max(jlo, (int)floorf(a)); jhi = min(jhi, (int)ceilf(b));
-                } else if (fabsf(fi * sin_t) >= lim) { jlo = 1; jhi = 0; }
-                if (fabsf(sin_t) > 1e-9f) {
-                    float a = (-fi * cos_t - lim) * inv_st, b = (-fi * cos_t + lim) * inv_st;
-                    if (a > b) { const float t2 = a; a = b; b = t2; }
-                    a = fminf(fmaxf(a, -cap), cap); b = fminf(fmaxf(b, -cap), cap);
-                    jlo = max(jlo, (int)floorf(a)); jhi = min(jhi, (int)ceilf(b));
-                } else if (fabsf(fi * cos_t) >= lim) { jlo = 1; jhi = 0; }
-                jlo = max(jlo, 1 - px); jhi = min(jhi, cols - 2 - px);
-                // trim the superset to the exact set: the float test below is monotone
-                // in j on each side (rotations of a row are monotone float sequences),
-                // so the accepted columns form one interval inside [jlo, jhi]
-                const float fi_s = (float)i * sin_t, fi_c = (float)i * cos_t;
-                auto inside = [&](int j) {
-                    const float cr = (float)j * cos_t - fi_s, rr2 = (float)j * sin_t + fi_c;
-                    const float rb = rr2 + (float)(DW / 2) - 0.5f, cb = cr + (float)(DW / 2) - 0.5f;
-                    return rb > -1.0f && rb < (float)DW && cb > -1.0f && cb < (float)DW;
-                };
-                while (jlo <= jhi && !inside(jlo)) ++jlo;
-                while (jhi >= jlo && !inside(jhi)) --jhi;
-            }
-            // row length for now (prefixed below), first column in the high half
-            rtab[rr] = (uint32_t)(jhi >= jlo ? jhi - jlo + 1 : 0) | ((uint32_t)(uint16_t)(int16_t)jlo << 16);
-        }
-        __syncthreads();
-        {   // wave-parallel exclusive prefix over the rows (<= 2*RMAX+1): lane owns a chunk of rows
-            constexpr int PER_MAX = (2 * VO_SIFT_DESCR_RMAX + 1 + 63) / 64;
-            const int per = (nrows + 63) >> 6, r0w = lane * per;
-            uint32_t ent[PER_MAX];
-            int sum = 0;
-#pragma unroll
-            for (int q = 0; q < PER_MAX; ++q) {
-                ent[q] = (q < per && r0w + q < nrows) ? rtab[r0w + q] : 0u;
-                sum += (int)(ent[q] & 0xFFFFu);
-            }
-            const int inc = wave_incl_scan(sum);
-            int acc = inc - sum;
-#pragma unroll
-            for (int q = 0; q < PER_MAX; ++q)
-                if (q < per && r0w + q < nrows) { rtab[r0w + q] = (uint32_t)acc | (ent[q] & 0xFFFF0000u); acc += (int)(ent[q] & 0xFFFFu); }
-            if (lane == 63) rtab[nrows] = (uint32_t)inc;
-            if (lane < 8) rtab[nrows + 1 + lane] = 0xFFFFu;
-        }
-        __syncthreads();
+        desc_tables(py, q, dcap, dyn, dyn + dt_rtab_off(), reinterpret_cast<float*>(dyn + dt_wtab_off(dcap)), lane);
+        const int o = __builtin_amdgcn_readfirstlane((int)hdr[DT_O]), layer = __builtin_amdgcn_readfirstlane((int)hdr[DT_LAYER]);
+        const OctGeom& g = py->oct[o];
+        const int P = g.pitch;
+        const float* gim = arena + g.g_off[layer] + img * py->istride;
+        const float ori = __uint_as_float(hdr[DT_ORI]);
+        const int px = (int)hdr[DT_PX], pyy = (int)hdr[DT_PY], radius = (int)hdr[DT_RADIUS];
+        const float cos_t = __uint_as_float(hdr[DT_COS]), sin_t = __uint_as_float(hdr[DT_SIN]);
 #if defined(VO_DESC_DIAG) && VO_DESC_DIAG >= 1
         const int nsamp = 0;                         // diagnostic build (timing only): no sample loop
 #else
-        const int nsamp = (int)rtab[nrows];
+        const int nsamp = (int)hdr[DT_NSAMP];
 #endif
         uint32_t* hc = hfx + (lane & (DCOPIES - 1)) * DCS;
         // one sample: weights, bins, fixed-point LDS atomics
@@ -2198,6 +2274,7 @@ static void sift_enqueue_small(const Pyramid& py, SiftBuffers& b, int n_img, hip
 {
     const SmallPlan sp = small_plan(py);
     if (sp.o_small >= py.n_oct) return;
+
     raise_lds_limit((const void*)k_small_pyr);
     VO_LAUNCH_NAMED("k_blur_small", k_small_pyr, dim3(n_img), dim3(VO_SMALL_T), sp.lds, s, d_py, b.arena, sp.o_small,
                     sp.rtab);
@@ -2345,21 +2422,21 @@ void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const v
     float* A = b.arena;
     const dim3 gs(py.n_seg > 0 ? py.n_seg : 1, n_img);
     VO_LAUNCH(k_seg_count, gs, dim3(256), 0, s, b.mask, b.woff, py.n_words, py.n_seg);
-    VO_LAUNCH(k_seg_scan, dim3(n_img), dim3(1024), 0, s, b.woff, b.n_cand, py.n_seg);
+    VO_LAUNCH(k_seg_scan, dim3(n_img), dim3(1024), 0, s, b.woff, b.n_cand, b.n_acc, py.n_seg);
     VO_LAUNCH(k_seg_emit, gs, dim3(256), 0, s, d_py, b.mask, (const uint32_t*)b.woff, b.cand, b.cand_cap);
-    VO_LAUNCH(k_refine, dim3(VO_REFINE_BLOCKS), dim3(256), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.cand_cap, n_img,
+    VO_LAUNCH(k_refine, dim3(VO_REFINE_BLOCKS), dim3(256), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.acc, b.n_acc, b.cand_cap, n_img,
               p.contrast_threshold, p.edge_threshold, p.sigma);
     const size_t fpre_bytes = sizeof(int) * (size_t)(n_img + 1);
-    VO_LAUNCH_NAMED("k_orient", (k_orient<36>), dim3(kFeatureGrid), dim3(64), fpre_bytes, s, d_py, A, b.n_cand,
+    const int* n_walk = VO_ACC_LIST ? b.n_acc : b.n_cand;    // the accepted list, or every candidate
+    VO_LAUNCH_NAMED("k_orient", (k_orient<36>), dim3(kFeatureGrid), dim3(64), fpre_bytes, s, d_py, A, n_walk, b.acc,
                     b.cout, b.cand_cap, n_img);
     VO_LAUNCH(k_scan_cands, dim3(n_img), dim3(1024), 0, s, b.cout, b.n_cand, b.koff, b.n_kp, b.cand_cap);
-    VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, b.n_cand, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
+    VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, n_walk, b.acc, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
                        n_img, p.upsample);
+    const size_t dt_bytes = sizeof(uint32_t) * (size_t)dt_stride(py.dcap);
     // 4 histogram copies: 2 -> +4 %, 8 -> +33 % k_desc time (MI355X)
-    const int rcap = desc_radius_cap(py, p);
-    VO_LAUNCH_NAMED("k_desc", (k_desc<VO_DESC_COPIES>), dim3(kFeatureGrid), dim3(64),
-                    sizeof(uint32_t) * (size_t)(3 * rcap + 11) + fpre_bytes, s, d_py, A, b.kpi, b.n_kp, b.desc,
-                    b.meta, b.kp_cap, n_img, rcap);
+    VO_LAUNCH_NAMED("k_desc", (k_desc<VO_DESC_COPIES>), dim3(kFeatureGrid), dim3(64), dt_bytes + fpre_bytes, s, d_py, A,
+                    b.kpi, b.n_kp, b.desc, b.meta, b.kp_cap, n_img);
 }
 
 void sift_enqueue(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img, const vo_sift_params& p,

@@ -78,7 +78,27 @@ struct Pyramid {
     int estrips[VO_SIFT_MAX_OCTAVES];         // strips per row in octave o
     int n_units;                              // units per image
     int n_seg;                                // 1024-word compaction segments per image
+    int dcap;                                 // largest descriptor window radius the parameters allow
 };
+
+// Feature-stage build switch (A/B builds; the product uses the default):
+//  VO_ACC_LIST   1: k_refine lists the accepted candidates and k_orient / k_expand walk the list
+#ifndef VO_ACC_LIST
+#define VO_ACC_LIST 1
+#endif
+//  VO_FEAT_PREFETCH 1: k_desc loads the next keypoint's record one iteration ahead
+#ifndef VO_FEAT_PREFETCH
+#define VO_FEAT_PREFETCH 0
+#endif
+
+// k_desc's per-keypoint window tables in LDS (desc_tables), u32 words: a header of DT_HDR words
+// (DT_ORI .. DT_LAYER below), the row table (2 dcap + 10 entries) and the separable window
+// weights (dcap + 1 floats); stride rounded to 16 B.
+#define DT_HDR 12
+enum { DT_ORI, DT_PX, DT_PY, DT_RADIUS, DT_COS, DT_SIN, DT_NSAMP, DT_NROWS, DT_O, DT_LAYER };
+static inline __host__ __device__ int dt_rtab_off() { return DT_HDR; }
+static inline __host__ __device__ int dt_wtab_off(int dcap) { return DT_HDR + 2 * dcap + 10; }
+static inline __host__ __device__ int dt_stride(int dcap) { return (DT_HDR + 3 * dcap + 11 + 3) & ~3; }
 
 #ifndef VO_EXT_BAND
 #define VO_EXT_BAND 30            // interior rows per extremum-test wave (a multiple of 3)
@@ -121,6 +141,8 @@ struct SiftBuffers {
     uint32_t* woff = nullptr;          // [n_img][n_seg] segment counts, then exclusive offsets
     uint32_t* cand = nullptr;          // [n_img][cand_cap]
     int* n_cand = nullptr;             // [n_img]  (uncapped count)
+    int* acc = nullptr;                // [n_img][cand_cap] accepted candidates' indices (k_refine, any order)
+    int* n_acc = nullptr;              // [n_img]
     CandOut* cout = nullptr;           // [n_img][cand_cap]
     uint32_t* koff = nullptr;          // [n_img][cand_cap]
     int* n_kp = nullptr;               // [n_img]  (uncapped count)
