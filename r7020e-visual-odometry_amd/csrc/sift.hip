@@ -1926,29 +1926,10 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
     const int lane = threadIdx.x;
     const long total = flat_setup(n_kp, kp_cap, n_img, fpre);
     const float bins_per_deg = (float)DN / 360.0f;
-#if VO_FEAT_PREFETCH
-    // the next keypoint's record is loaded one iteration ahead, so its latency overlaps this
-    // keypoint's work instead of heading the next one's table build
-    int img_n = 0, k_n = 0;
-    KpInt q_n{};
-    if (blockIdx.x < total) {
-        flat_find_wave(fpre, n_img, blockIdx.x, img_n, k_n);
-        q_n = kpi[(size_t)img_n * kp_cap + k_n];
-    }
-#endif
     for (long t = blockIdx.x; t < total; t += gridDim.x) {
         int img, k;
-#if VO_FEAT_PREFETCH
-        img = img_n; k = k_n;
-        const KpInt q = q_n;
-        if (t + gridDim.x < total) {
-            flat_find_wave(fpre, n_img, t + gridDim.x, img_n, k_n);
-            q_n = kpi[(size_t)img_n * kp_cap + k_n];
-        }
-#else
         flat_find_wave(fpre, n_img, t, img, k);
         const KpInt q = kpi[(size_t)img * kp_cap + k];
-#endif
         static_assert((DCOPIES * DCS) % 4 == 0, "16-B zeroing");
         typedef uint32_t u4z_t __attribute__((ext_vector_type(4)));
         for (int b = 4 * lane; b < DCOPIES * DCS; b += 256) *reinterpret_cast<u4z_t*>(&hfx[b]) = u4z_t{0u, 0u, 0u, 0u};

@@ -86,10 +86,7 @@ struct Pyramid {
 #ifndef VO_ACC_LIST
 #define VO_ACC_LIST 1
 #endif
-//  VO_FEAT_PREFETCH 1: k_desc loads the next keypoint's record one iteration ahead
-#ifndef VO_FEAT_PREFETCH
-#define VO_FEAT_PREFETCH 0
-#endif
+
 
 // k_desc's per-keypoint window tables in LDS (desc_tables), u32 words: a header of DT_HDR words
 // (DT_ORI .. DT_LAYER below), the row table (2 dcap + 10 entries) and the separable window
