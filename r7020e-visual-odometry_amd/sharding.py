@@ -71,7 +71,9 @@ def gather_frames(local: np.ndarray, n_frames: int, group=None, device=None) -> 
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    local = np.asarray(local, np.float64).reshape(len(local), -1)
+    local = np.asarray(local, np.float64)
+    if local.ndim != 2:                          # (a rank may own no frames: n < world)
+        local = local.reshape(len(local), -1)
     W = local.shape[1]
     maxn = max(shard_range(n_frames, world, r)[1] - shard_range(n_frames, world, r)[0] for r in range(world))
     buf = torch.zeros((maxn, W), dtype=torch.float64, device=device)

@@ -67,7 +67,7 @@ def _run(world, path):
     procs = [ctx.Process(target=_worker, args=(r, world, port, str(path), q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = q.get(timeout=600)
+    res = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -105,8 +105,9 @@ def street_seq(tmp_path_factory, oracle):
     return path, outs, lm
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_street_sequence_poses_and_landmarks_equal_single_process(street_seq, world):
+    """world 8 (the configs[3] node) over 6 frames also leaves ranks 6 and 7 without frames."""
     path, outs, lm = street_seq
     assert (outs["status"][1:] == 0).all() and len(lm) > 100
     _check(_run(world, path), outs, lm)

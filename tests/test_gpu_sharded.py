@@ -76,11 +76,12 @@ def test_sharded_libvo_equals_single_run(vo, street_seq, single_run, world):
     assert lm.shape == lm1.shape and np.array_equal(lm, lm1)
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 10])
 def test_device_world_transform_of_shards_equals_single_run(vo, street_seq, single_run, world):
     """kitti.finish_shard's per-rank step: each shard's own rows moved to the world on the device
     (vo_landmarks_world_dev, k_lm_world) with the chained poses of its frames, halo frame
-    included; the shards' float32 rows concatenated in rank order equal the single run's map."""
+    included; the shards' float32 rows concatenated in rank order equal the single run's map.
+    (world 10 over 8 frames: two ranks own no frame and run only their halo.)"""
     import torch
     from r7020e_visual_odometry_amd import kitti, sharding
     L, R, P0, P1, _ = street_seq
