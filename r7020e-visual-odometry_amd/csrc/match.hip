@@ -244,7 +244,9 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
             __syncthreads();                               // tile jt visible; tile jt-32's buffer free
             if (jt + 32 < j1) {
                 lstore(buf ^ 1);                           // tile jt+32 (loaded one iteration ago)
-                if (jt + 64 < j1) gload(jt + 64);
+#if !(defined(VO_MATCH_DIAG) && VO_MATCH_DIAG == 2)
+                if (jt + 64 < j1) gload(jt + 64);          // (diagnostic build 2: no F2 loads after the first)
+#endif
             }
             v4i b[4];
             const uint8_t* brow = &bt[buf][l31 * MP_LDS_ROW + 16 * h];
@@ -259,6 +261,10 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
             // ragged last tile: masked columns get c = -inf (never ranked); elsewhere c + 0 = c
             // exactly (c >= +0)
             const float cmask = jc < j1 ? 0.0f : -INFINITY;
+#if defined(VO_MATCH_DIAG) && VO_MATCH_DIAG == 1
+            // diagnostic build 1 (timing only): no epilogue, the accumulators feed one running max
+            for (int reg = 0; reg < 16; ++reg) best[reg] = fmaxf(best[reg], (float)accv[reg] + cmask);
+#else
 #pragma unroll
             for (int reg = 0; reg < 16; reg += 2) {
                 // c for two accumulator rows at once: the two products as packed f32 muls
@@ -278,6 +284,7 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
                     }
                 }
             }
+#endif
             ++tno;
             if ((tno & (tno - 1)) == 0) {                  // wave-uniform
 #pragma unroll

@@ -178,12 +178,20 @@ def load_library(path: str | os.PathLike | None = None):
     return L
 
 
+def experimental_library_path() -> Path:
+    """libvo_exp.so beside the product library in use: the in-tree test build, or -- when
+    $VO_LIBPATH points at another libvo.so (a variant build) -- the libvo_exp.so next to it, so an
+    experimental cross-check compares a build with its own test build."""
+    lp = os.environ.get("VO_LIBPATH")
+    return Path(lp).resolve().parent / "libvo_exp.so" if lp else EXP_LIBPATH
+
+
 def load_experimental_library():
-    """The test build libvo_exp.so (see EXP_LIBPATH) with `vo_exp_set(fused_octave, msac_eager)`
-    bound; pass it to Context(lib=...)."""
-    L = load_library(EXP_LIBPATH)
+    """The test build libvo_exp.so (experimental_library_path()) with `vo_exp_set(fused_octave,
+    msac_eager)` bound; pass it to Context(lib=...).  Raises VOError if it is not built."""
+    L = load_library(experimental_library_path())
     if not hasattr(L, "vo_exp_set"):
-        raise VOError(VO_ERR_STATE, f"{EXP_LIBPATH} lacks vo_exp_set (not a VO_EXPERIMENTAL build)")
+        raise VOError(VO_ERR_STATE, f"{experimental_library_path()} lacks vo_exp_set (not a VO_EXPERIMENTAL build)")
     L.vo_exp_set.argtypes = [C.c_int, C.c_int]
     return L
 

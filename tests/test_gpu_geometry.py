@@ -2,6 +2,8 @@
 oracle: find_remaining_points (index sets), triangulate (f64 bit-exact),
 estworldpose (pose bit-exact, inlier masks bit-exact), landmarks, and the whole
 VO.m loop over a synthetic sequence (batched and frame-by-frame)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -92,6 +94,8 @@ def test_estworldpose_lazy_chunks_equal_oracle_and_eager(vo, oracle, outlier_fra
     orp = oracle.ransac_params()
     orp.max_num_trials = max_trials
     ref = oracle.estworldpose(uv, Xw, K, params=orp, frame_key=7)
+    if os.environ.get("VO_LIBPATH") and not vo.experimental_library_path().exists():
+        pytest.skip("variant build without its own libvo_exp.so")
     exp = vo.load_experimental_library()
     for eager, lib in ((0, None), (1, exp)):
         ctx = vo.Context(375, 1242, 1, ransac=rp, lib=lib)
