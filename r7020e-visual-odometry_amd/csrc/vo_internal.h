@@ -88,6 +88,7 @@ struct Pyramid {
 #endif
 
 
+
 // k_desc's per-keypoint window tables in LDS (desc_tables), u32 words: a header of DT_HDR words
 // (DT_ORI .. DT_LAYER below), the row table (2 dcap + 10 entries) and the separable window
 // weights (dcap + 1 floats); stride rounded to 16 B.
