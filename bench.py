@@ -157,7 +157,7 @@ def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks,
     ctx.close()
     del dL, dR
     fk_ms = {k: round(v[0] / PB, 4) for k, v in sorted(fkt.items(), key=lambda kv: -kv[1][0])}
-    geom = ("k_compose", "k_gather_tri", "k_msac", "k_stereo_pos", "k_lm_filter", "k_lm_tri", "k_lm_pack", "k_tri_list")
+    geom = ("k_compose", "k_gather_tri", "k_msac", "k_msac_gen", "k_stereo_pos", "k_lm_filter", "k_lm_tri", "k_lm_pack", "k_tri_list")
     # k_msac (lazy MSAC: slots generated and scored in chunks of 64 until the adaptive replay
     # stops -- one chunk at these inlier ratios): every scored slot reprojects every tracked
     # point -- R X + t (18), two divisions, K (6), residual and square (5), MSAC sum (1): 32 f64

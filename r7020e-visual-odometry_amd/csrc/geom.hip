@@ -59,10 +59,9 @@ hipError_t geom_alloc(GeomBuffers& g, int max_frames, int kp_cap, int n_hyp)
 
 void geom_free(GeomBuffers& g)
 {
-    hipFree(g.lists); hipFree(g.list_n); hipFree(g.step_i); hipFree(g.step_j); hipFree(g.step_n); hipFree(g.world);
-    hipFree(g.imgpt); hipFree(g.oldpos); hipFree(g.inliers); hipFree(g.hyp); hipFree(g.fg); hipFree(g.spos);
-    hipFree(g.s_n); hipFree(g.lm_new); hipFree(g.lm_M); hipFree(g.lm_X); hipFree(g.lm_keep); hipFree(g.lm_rows);
-    hipFree(g.lm_pX); hipFree(g.lm_pkeep);
+    void* bufs[] = {g.lists, g.list_n, g.step_i, g.step_j, g.step_n, g.world, g.imgpt, g.oldpos, g.inliers, g.hyp,
+                    g.fg, g.spos, g.s_n, g.lm_new, g.lm_M, g.lm_X, g.lm_keep, g.lm_rows, g.lm_pX, g.lm_pkeep};
+    for (void* p : bufs) (void)hipFree(p);   // teardown: nothing to report to
     g = GeomBuffers();
 }
 
@@ -254,28 +253,91 @@ __global__ void k_tri_list(const float* __restrict__ pos, int n, CalibDev cal, d
 // P3P (oracle_p3p) — Grunert's quartic by polynomial algebra, deterministic
 // bracketing/bisection root finder (template recursion = the oracle's).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double peval_dev(const double* a, int deg, double x)
+// Register-resident form: every array index is a compile-time constant (fixed-degree solvers
+// selected by a switch on the trimmed degree, roots appended through select chains), so the
+// coefficients, critical points and roots stay in VGPRs -- the dynamically indexed form
+// lived in scratch and its bisection loop waited on scratch loads every iteration.  Same
+// operations in the same order as the oracle (real_roots, oracle/vo_ref.c:294): the trim
+// keeps the largest i >= 1 with !(|a_i| <= 1e-14 amax), Horner as r = r*x + a_i.
+template <int D>
+__device__ __forceinline__ double peval_fixed(const double* a, double x)
 {
-    double r = a[deg];
-    for (int i = deg - 1; i >= 0; --i) r = r * x + a[i];
+    double r = a[D];
+#pragma unroll
+    for (int i = D - 1; i >= 0; --i) r = r * x + a[i];
     return r;
 }
 
-template <int MAXDEG>
-__device__ int real_roots_dev(const double* a_in, int deg, double* roots);
-
-template <>
-__device__ int real_roots_dev<1>(const double*, int, double*) { return 0; }
-
-template <int MAXDEG>
-__device__ int real_roots_dev(const double* a_in, int deg, double* roots)
+template <int N>
+__device__ __forceinline__ void push_root(double* r, int& nr, double v)
 {
-    double a[5];
-    for (int i = 0; i <= deg; ++i) a[i] = a_in[i];
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (i == nr) r[i] = v;
+    nr++;
+}
+
+template <int MAXD>
+__device__ int real_roots_trim(const double* a, double* roots);
+
+// one bracketed interval: an exact zero at lo, or bisection to adjacent doubles (<= 200 halvings)
+template <int D, int N>
+__device__ __forceinline__ void bisect_interval(const double* a, double lo, double hi, double* roots, int& nr,
+                                                double& last)
+{
+    double flo = peval_fixed<D>(a, lo), fhi = peval_fixed<D>(a, hi);
+    if (flo == 0.0) {
+        if (nr == 0 || last != lo) { push_root<N>(roots, nr, lo); last = lo; }
+        return;
+    }
+    if ((flo < 0) == (fhi < 0)) return;
+    for (int it = 0; it < 200; ++it) {
+        double mid = 0.5 * (lo + hi);
+        if (mid <= lo || mid >= hi) break;
+        double fm = peval_fixed<D>(a, mid);
+        if (fm == 0.0) { lo = hi = mid; break; }
+        if ((fm < 0) == (flo < 0)) { lo = mid; flo = fm; } else hi = mid;
+    }
+    last = 0.5 * (lo + hi);
+    push_root<N>(roots, nr, last);
+}
+
+// exact degree D >= 3: critical points from the derivative, then one bisection per bracket
+template <int D>
+__device__ __forceinline__ int real_roots_fixed(const double* a, double* roots)
+{
+    double d[D];
+#pragma unroll
+    for (int i = 1; i <= D; ++i) d[i - 1] = a[i] * (double)i;
+    double crit[D - 1];
+    const int nc = real_roots_trim<D - 1>(d, crit);
+    double B = 0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) { double t = fabs(a[i] / a[D]); if (t > B) B = t; }
+    B = B + 1.0;
+    int nr = 0;
+    double last = 0.0, prev = -B;
+#pragma unroll
+    for (int k = 0; k < D - 1; ++k) {
+        if (k < nc && crit[k] > -B && crit[k] < B) {
+            bisect_interval<D, D>(a, prev, crit[k], roots, nr, last);
+            prev = crit[k];
+        }
+    }
+    bisect_interval<D, D>(a, prev, B, roots, nr, last);
+    return nr;
+}
+
+template <int MAXD>
+__device__ int real_roots_trim(const double* a, double* roots)
+{
     double amax = 0;
-    for (int i = 0; i <= deg; ++i) if (fabs(a[i]) > amax) amax = fabs(a[i]);
+#pragma unroll
+    for (int i = 0; i <= MAXD; ++i) if (fabs(a[i]) > amax) amax = fabs(a[i]);
     if (amax == 0.0) return 0;
-    while (deg > 0 && fabs(a[deg]) <= 1e-14 * amax) deg--;
+    int deg = 0;
+#pragma unroll
+    for (int i = 1; i <= MAXD; ++i) if (!(fabs(a[i]) <= 1e-14 * amax)) deg = i;
     if (deg == 0) return 0;
     if (deg == 1) { roots[0] = -a[0] / a[1]; return 1; }
     if (deg == 2) {
@@ -287,34 +349,13 @@ __device__ int real_roots_dev(const double* a_in, int deg, double* roots)
         if (r1 <= r2) { roots[0] = r1; roots[1] = r2; } else { roots[0] = r2; roots[1] = r1; }
         return 2;
     }
-    double d[4] = {0, 0, 0, 0};
-    for (int i = 1; i <= deg; ++i) d[i - 1] = a[i] * (double)i;
-    double crit[4];
-    int nc = real_roots_dev<MAXDEG - 1>(d, deg - 1, crit);
-    double B = 0;
-    for (int i = 0; i < deg; ++i) { double t = fabs(a[i] / a[deg]); if (t > B) B = t; }
-    B = B + 1.0;
-    double pts[6];
-    int np = 0;
-    pts[np++] = -B;
-    for (int i = 0; i < nc; ++i) if (crit[i] > -B && crit[i] < B) pts[np++] = crit[i];
-    pts[np++] = B;
-    int nr = 0;
-    for (int k = 0; k + 1 < np; ++k) {
-        double lo = pts[k], hi = pts[k + 1];
-        double flo = peval_dev(a, deg, lo), fhi = peval_dev(a, deg, hi);
-        if (flo == 0.0) { if (nr == 0 || roots[nr - 1] != lo) roots[nr++] = lo; continue; }
-        if ((flo < 0) == (fhi < 0)) continue;
-        for (int it = 0; it < 200; ++it) {
-            double mid = 0.5 * (lo + hi);
-            if (mid <= lo || mid >= hi) break;
-            double fm = peval_dev(a, deg, mid);
-            if (fm == 0.0) { lo = hi = mid; break; }
-            if ((fm < 0) == (flo < 0)) { lo = mid; flo = fm; } else hi = mid;
-        }
-        roots[nr++] = 0.5 * (lo + hi);
+    if constexpr (MAXD >= 4) {
+        if (deg == 4) return real_roots_fixed<4>(a, roots);
     }
-    return nr;
+    if constexpr (MAXD >= 3) {
+        return real_roots_fixed<3>(a, roots);
+    }
+    return 0;
 }
 
 __device__ __forceinline__ void pmul_dev(const double* a, int da, const double* b, int db, double* out)
@@ -420,10 +461,12 @@ __device__ int p3p_hyp_dev(const double im3[3][2], const double w3[3][3], const 
         P[i] = v;
     }
     double roots[4];
-    int nr = real_roots_dev<4>(P, 4, roots);
+    const int nr = real_roots_trim<4>(P, roots);
     int ns = 0, best = -1;
     double be = INFINITY;
-    for (int k = 0; k < nr; ++k) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k >= nr) break;
         double v = roots[k];
         if (!(v > 0)) continue;
         double Dv = D[0] + D[1] * v;
@@ -640,8 +683,30 @@ __device__ void msac_final(const MsacArgs& a, int f, int n, int best, int status
 // -- and stops at the chunk where the replay stops.  At the ~97 % inlier ratios of the KITTI
 // path the replay needs ~3 trials, so one chunk of 64 replaces 2048 eager slots.  Same
 // slots, same per-slot arithmetic, same replay: results identical to the eager kernels.
-#define VO_MSAC_CHUNK 64
+#ifndef VO_MSAC_CHUNK
+#define VO_MSAC_CHUNK 64          // slots per chunk after the first (<= 64: one lane per slot)
+#endif
+#ifndef VO_MSAC_FIRST
+#define VO_MSAC_FIRST 64          // slots of the first chunk (<= VO_MSAC_CHUNK)
+#endif
+#ifndef VO_MSAC_T
 #define VO_MSAC_T 1024            // 16 waves: a chunk's 64 slots scored 4 per wave (one block per frame)
+#endif
+#ifndef VO_MSAC_SPLITGEN
+#define VO_MSAC_SPLITGEN 0        // 1: the first chunk's hypotheses come from k_msac_gen (64-lane blocks)
+#endif
+
+#if VO_MSAC_SPLITGEN
+// first chunk of every frame, one lane per slot: a 64-thread block has the whole register file
+// for the P3P root finder that spills at k_msac's 1024-thread bound
+__global__ __launch_bounds__(64) void k_msac_gen(MsacArgs a)
+{
+    const int f = blockIdx.x, s = threadIdx.x;
+    const int limit = a.max_trials < a.n_hyp ? a.max_trials : a.n_hyp;
+    if (s < VO_MSAC_FIRST && s < limit) msac_hyp_slot(a, f, s, msac_n(a, f));
+}
+#endif
+
 __global__ __launch_bounds__(VO_MSAC_T) void k_msac(MsacArgs a)
 {
     __shared__ int s_best, s_status, s_done;
@@ -654,9 +719,9 @@ __global__ __launch_bounds__(VO_MSAC_T) void k_msac(MsacArgs a)
     double best_score = INFINITY;
     if (tid == 0) s_done = n < 4;
     __syncthreads();
-    for (int c0 = 0; !s_done && c0 < limit; c0 += VO_MSAC_CHUNK) {
-        const int c1 = min(c0 + VO_MSAC_CHUNK, limit);
-        if (tid < c1 - c0) msac_hyp_slot(a, f, c0 + tid, n);
+    for (int c0 = 0, c1 = min(VO_MSAC_FIRST, limit); !s_done && c0 < limit;
+         c0 = c1, c1 = min(c1 + VO_MSAC_CHUNK, limit)) {
+        if (tid < c1 - c0 && (!VO_MSAC_SPLITGEN || c0 > 0)) msac_hyp_slot(a, f, c0 + tid, n);
         __syncthreads();                                    // the chunk's slots are written
         for (int s = c0 + wv; s < c1; s += VO_MSAC_T / 64)
             if (a.hyp[(size_t)f * a.n_hyp + s].valid) msac_score_slot(a, f, s, n, lane);
@@ -869,6 +934,9 @@ static void msac_enqueue(const MsacArgs& a, int B, hipStream_t s)
         VO_LAUNCH(k_msac_select, dim3(B), dim3(64), 0, s, a);
         return;
     }
+#endif
+#if VO_MSAC_SPLITGEN
+    VO_LAUNCH(k_msac_gen, dim3(B), dim3(64), 0, s, a);
 #endif
     VO_LAUNCH(k_msac, dim3(B), dim3(VO_MSAC_T), 0, s, a);
 }

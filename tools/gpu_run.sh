@@ -71,7 +71,7 @@ for st in $STEPS; do
     for var in default ${v//,/ } default; do
       if [ $var = default ]; then unset VO_LIBPATH; else export VO_LIBPATH=$GRAFT_REPO_ROOT/tools/variants/$var/libvo.so; fi
       timeout -k 10 300 python3 bench.py --no-cpu --large-batch 0 > $O/abf_$var.json 2>/dev/null || { echo "$var failed"; exit 1; }
-      python3 -c "import json;d=json.load(open('$O/abf_$var.json'));f=d['full_path'];print('$var',round(d['value'],1),round(d['ms_per_step'],3),'full',round(f['value'],1),'refine',d['roofline']['kernel_ms_per_step'].get('k_refine'),f['kernel_ms_per_step'].get('k_refine'))"
+      python3 -c "import json;d=json.load(open('$O/abf_$var.json'));f=d['full_path'];k=f['kernel_ms_per_step'];print('$var',round(d['value'],1),round(d['ms_per_step'],3),'full',round(f['value'],1),'refine',d['roofline']['kernel_ms_per_step'].get('k_refine'),k.get('k_refine'),'msac',k.get('k_msac'),k.get('k_msac_gen'))"
     done
     unset VO_LIBPATH ;;
   ab:*)
