@@ -20,7 +20,7 @@ per-frame records all-gathered, poses chained on every rank, each rank's landmar
 rows moved to the world on its device and gathered to rank 0; it reports the reference's lagged xz error
 (PlotOnMap.m:8-20) and ATE against that trajectory (--seq-frames; 0 skips), and
 `large` the 1920x1080 / ~8k keypoint configuration (configs[4]) per GPU with the
-i8-MFMA rate of its dense stereo match block (--large-batch, default 8; 0 skips).
+i8-MFMA rate of its dense stereo match block (--large-batch, default 64; 0 skips).
 """
 from __future__ import annotations
 
@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--seq-batch", type=int, default=64, help="frames per vo_step_submit_dev call in the sequence leg")
     ap.add_argument("--dry-run", action="store_true",
                     help="rendezvous only (gloo, no GPU): rank 0 prints the world size it sees (launcher test)")
-    ap.add_argument("--large-batch", type=int, default=8,
+    ap.add_argument("--large-batch", type=int, default=64,
                     help="1920x1080 (~8k keypoints) stereo pairs per step for the configs[4] figure (0: skip)")
     return ap.parse_args()
 
@@ -288,7 +288,8 @@ def main():
     B = args.batch
     # synthetic pairs: rank r renders frames [r*B, (r+1)*B) (seed 0x5EED0000 + frame); texture
     # cell of 15 px puts the oracle at ~2000 keypoints per image (2000 +- 200)
-    L, R = syn.independent_pairs(B, ROWS, COLS, first=rank * B, px_per_cell=syn.BENCH_PX_PER_CELL)
+    L, R = syn.independent_pairs(B, ROWS, COLS, first=rank * B, px_per_cell=syn.BENCH_PX_PER_CELL,
+                                 threads=args.cpu_threads)
     d_l = torch.from_numpy(L).to(f"cuda:{local}")
     d_r = torch.from_numpy(R).to(f"cuda:{local}")
     torch.cuda.synchronize()
@@ -411,7 +412,7 @@ def main():
     large = None
     if args.large_batch > 0:
         LB = args.large_batch
-        GL, GR = syn.large_pairs(LB, first=rank * LB)
+        GL, GR = syn.large_pairs(LB, first=rank * LB, threads=args.cpu_threads)
         d_gl = torch.from_numpy(GL).to(f"cuda:{local}")
         d_gr = torch.from_numpy(GR).to(f"cuda:{local}")
         lctx = vo.Context(syn.LARGE_ROWS, syn.LARGE_COLS, LB, device=local)

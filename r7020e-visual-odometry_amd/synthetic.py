@@ -159,19 +159,30 @@ def stereo_pair(seed: int, rows: int = 375, cols: int = 1242, noise_sd: float = 
 
 
 def independent_pairs(n: int, rows: int = 375, cols: int = 1242, first: int = 0,
-                      px_per_cell: float = 16.0):
-    """n independent stereo pairs; frame f uses seed 0x5EED0000 + f. -> (L, R) [n, rows, cols] u8."""
+                      px_per_cell: float = 16.0, threads: int = 1):
+    """n independent stereo pairs; frame f uses seed 0x5EED0000 + f. -> (L, R) [n, rows, cols] u8.
+    `threads` > 1 renders pairs concurrently (numpy releases the GIL in its array loops); every
+    pair depends on its seed alone, so the result does not depend on `threads`."""
     L = np.empty((n, rows, cols), np.uint8)
     R = np.empty((n, rows, cols), np.uint8)
-    for i in range(n):
+
+    def one(i):
         seed = SEED_BASE + first + i
         L[i], R[i] = stereo_pair(seed, rows, cols, planes=random_scene(seed, rows, cols, px_per_cell=px_per_cell))
+
+    if threads > 1 and n > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(min(threads, n)) as ex:
+            list(ex.map(one, range(n)))
+    else:
+        for i in range(n):
+            one(i)
     return L, R
 
 
-def large_pairs(n: int, first: int = 0):
+def large_pairs(n: int, first: int = 0, threads: int = 1):
     """BASELINE configs[4] inputs: n independent 1920x1080 pairs with ~8k keypoints per image."""
-    return independent_pairs(n, LARGE_ROWS, LARGE_COLS, first, LARGE_PX_PER_CELL)
+    return independent_pairs(n, LARGE_ROWS, LARGE_COLS, first, LARGE_PX_PER_CELL, threads)
 
 
 def yaw(deg: float) -> np.ndarray:

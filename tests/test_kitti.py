@@ -128,3 +128,11 @@ def test_reference_error_curve_fixture():
     assert abs(d[-1, 0] - t[-1]) < 1.0
     assert 40.0 < d[:, 1].max() < 41.5 and 450 < d[np.argmax(d[:, 1]), 0] < 470
     assert 34.0 < d[-1, 1] < 35.3 and 13.5 < d[:, 1].mean() < 15.0
+
+
+def test_threaded_pair_rendering_equals_serial(syn):
+    """bench.py renders its synthetic pairs on --cpu-threads threads: every pair depends on its
+    seed alone, so the images are the serial ones."""
+    L1, R1 = syn.independent_pairs(6, 48, 80, first=3)
+    L4, R4 = syn.independent_pairs(6, 48, 80, first=3, threads=4)
+    assert np.array_equal(L1, L4) and np.array_equal(R1, R4)
