@@ -4,7 +4,8 @@
 Workload (BASELINE.json configs[1]): SIFT detect+describe of both images +
 stereo matchFeatures, on 1242x375 synthetic stereo pairs (~2k keypoints per
 image), via libvo.so (hand-written HIP, gfx950).  One step = one batch of
-`--batch` independent stereo frames already resident in HBM.  With --gpus N
+`--batch` independent stereo frames already resident in HBM (default 128, the
+library's largest batch: +1.4 % over 64 on one box, profiles/r05_o_batch.txt).  With --gpus N
 (one process per GPU, RCCL; under torchrun, or bench.py starts torchrun itself
 when WORLD_SIZE is unset) each rank processes its own frames: weak scaling, no
 data-path collective; value = all frames / max-over-ranks time.
@@ -50,10 +51,10 @@ TRAFFIC_FILE = max(ROOT.glob("profiles/r*_pmc_traffic.json"), default=ROOT / "pr
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20, help="timed steps per run (64 frames each: 1280 frames per run)")
+    ap.add_argument("--steps", type=int, default=20, help="timed steps per run (--batch frames each: 2560 frames per run at 128)")
     ap.add_argument("--runs", type=int, default=5, help="timed runs of --steps steps; value = the median run (SURVEY §8d)")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64, help="stereo frames per step")
+    ap.add_argument("--batch", type=int, default=128, help="stereo frames per step (library maximum 128)")
     ap.add_argument("--cpu-frames", type=int, default=32, help="frames in the CPU-oracle baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline (the box's share)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -481,7 +482,7 @@ def main():
         line = {
             "metric": "stereo frames/sec @1242x375 (SIFT detect+describe x2 + stereo matchFeatures)",
             "value": fps, "unit": "stereo frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms_per_step, "timed_runs": timed_runs, "h2d": h2d_line,
+            "ms_per_step": ms_per_step, "ms_per_64_frames": ms_per_step * 64 / B, "timed_runs": timed_runs, "h2d": h2d_line,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32 (i8 MFMA for exact descriptor dot products)", "data": "synthetic",
             "config": {"workload": "BASELINE configs[1]: SIFT detect+describe + BF match on 1242x375 synthetic stereo, "

@@ -77,12 +77,16 @@ for st in $STEPS; do
   ab:*)
     v=${st#ab:}; timeout -k 10 900 bash tools/variant_bench.sh ${v//,/ } > $O/ab_${v//,/_}.txt 2>&1 || { cat $O/ab_${v//,/_}.txt; exit 1; }
     cat $O/ab_${v//,/_}.txt ;;
-  pmc)
+  pmc|pmc:*)
+    # pmc:<name> also installs the per-launch traffic as profiles/<name> in this box's copy, so a
+    # later bench step of the same call reads it (commit the merged gpurun_out copy afterwards)
     timeout -k 10 900 bash tools/pmc_passes.sh _$(basename $O) > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
+    python3 tools/pmc_traffic.py gpurun_out/pmc_$(basename $O) $O/pmc_traffic.json > /dev/null
+    [ "$st" != pmc ] && cp $O/pmc_traffic.json profiles/${st#pmc:}
     echo pmc-done ;;
   insitu)
     # kernel trace of the asynchronous loop + the counter passes -> tools/insitu_model.py
-    timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $O/itrace -o t -- python3 tools/prof_run.py 64 6 > $O/itrace.log 2>&1 \
+    timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $O/itrace -o t -- python3 tools/prof_run.py ${PMC_BATCH:-128} 6 > $O/itrace.log 2>&1 \
       || { tail -20 $O/itrace.log; exit 1; }
     timeout -k 10 900 bash tools/pmc_passes.sh _$(basename $O) > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
     python3 tools/insitu_model.py gpurun_out/pmc_$(basename $O) $(find $O/itrace -name "*kernel_trace.csv" | head -1) $O/insitu.json
