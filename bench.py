@@ -347,7 +347,7 @@ def main():
     h2d_line = {"bytes_per_step": h2d_bytes, "ms_per_step": h2d, "gb_s": h2d_bytes / (h2d * 1e-3) / 1e9,
                 "frames_per_s_serial_computed": B / ((ms_per_step + h2d) * 1e-3),
                 "frames_per_s_overlapped_computed": B / (max(ms_per_step, h2d) * 1e-3),
-                "note": "measured: the pinned host -> HBM copy of the step's 2x64 u8 images (torch, one stream), "
+                "note": f"measured: the pinned host -> HBM copy of the step's 2x{B} u8 images (torch, one stream), "
                         "median of 5.  COMPUTED, not measured: serial = 1 / (copy + compute), overlapped = "
                         "1 / max(copy, compute) (copy of step N+1 beside compute of step N)"}
 
