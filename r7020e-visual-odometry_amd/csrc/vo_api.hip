@@ -644,6 +644,13 @@ static SetRef set_ref(vo_ctx* c, int set)
 #ifndef VO_EXT_SPLIT
 #define VO_EXT_SPLIT 1
 #endif
+// Where the LDS-sized octaves (k_small_pyr: one 1024-thread workgroup per image, ~120 KB of LDS)
+// run: 0 at the scale space's tail, 1 at the head of the feature stream's second part (after
+// ev_join, before the extremum test of octaves 1..), where the previous batch's descriptor
+// waves no longer hold the CUs' LDS.
+#ifndef VO_SMALL_ON_FEATURE
+#define VO_SMALL_ON_FEATURE 0
+#endif
 static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uint8_t* d_r, int B, bool join,
                                bool fork = true)
 {
@@ -664,7 +671,8 @@ static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uin
         ImageSrc src{d_l + f0 * fs, d_r + f0 * fs, fs, c->cols, 0};
         SiftBuffers v = sift_view(*S.sb, c->py, 2 * f0, 2 * nf);
         sift_enqueue_pyramid(c->py, v, src, 2 * nf, c->sp, sp, c->d_py, c->ev_o0[p]);
-        sift_enqueue_pyramid_tail(c->py, v, 2 * nf, c->sp, sp, c->d_py, VO_EXT_SPLIT ? c->py.n_oct : 1);
+        if (!VO_SMALL_ON_FEATURE)
+            sift_enqueue_pyramid_tail(c->py, v, 2 * nf, c->sp, sp, c->d_py, VO_EXT_SPLIT ? c->py.n_oct : 1);
         HIPC(c, hipEventRecord(c->ev_join[p], sp));
     }
     for (int p = 0; p < parts; ++p) {
@@ -675,6 +683,8 @@ static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uin
         HIPC(c, hipStreamWaitEvent(st, c->prof.on && join ? c->ev_join[p] : c->ev_o0[p], 0));
         sift_enqueue_extrema(c->py, v, 2 * nf, c->sp, st, c->d_py, 0, 1);
         HIPC(c, hipStreamWaitEvent(st, c->ev_join[p], 0));
+        if (VO_SMALL_ON_FEATURE)
+            sift_enqueue_pyramid_tail(c->py, v, 2 * nf, c->sp, st, c->d_py, VO_EXT_SPLIT ? c->py.n_oct : 1);
         if (VO_EXT_SPLIT) sift_enqueue_extrema(c->py, v, 2 * nf, c->sp, st, c->d_py, 1, c->py.n_oct);
         sift_enqueue_features(c->py, v, 2 * nf, c->sp, st, c->d_py);
         match_launch(match_view(*S.mb, f0), S.jobs + f0, nf, c->mp, st);
