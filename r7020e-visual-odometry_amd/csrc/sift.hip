@@ -2251,7 +2251,9 @@ static SmallPlan small_plan(const Pyramid& py)
 // scale-space stream after the last level blur (its workgroups need ~120 KB of one CU's LDS; by
 // then octave 0's extremum test has moved to the feature stream, so the previous batch's
 // descriptor waves no longer hold every CU's LDS when it arrives -- DESIGN.md §9c).
-static void sift_enqueue_small(const Pyramid& py, SiftBuffers& b, int n_img, hipStream_t s, const Pyramid* d_py)
+int sift_small_octave(const Pyramid& py) { return small_plan(py).o_small; }
+
+void sift_enqueue_small(const Pyramid& py, SiftBuffers& b, int n_img, hipStream_t s, const Pyramid* d_py)
 {
     const SmallPlan sp = small_plan(py);
     if (sp.o_small >= py.n_oct) return;

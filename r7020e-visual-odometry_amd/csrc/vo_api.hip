@@ -69,7 +69,7 @@ struct vo_ctx {
     static constexpr int MAX_SUB = 4;
     int n_sub = 1;
     hipStream_t sub[MAX_SUB] = {};                 // sub[0]: scale-space stream, sub[1]: feature stream
-    hipEvent_t ev_fork = nullptr, ev_join[MAX_SUB] = {}, ev_o0[MAX_SUB] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[MAX_SUB] = {}, ev_o0[MAX_SUB] = {}, ev_small[MAX_SUB] = {};
     // Asynchronous batch pipeline (vo_sift_match_batch_dev): calls alternate between two
     // buffer sets; set 0 is the context's own buffers (sb, mb, stereo jobs, pairs), set 1
     // is `aux`.  A call's scale space waits only for the previous use of its own set, so
@@ -192,7 +192,8 @@ static void destroy_streams(vo_ctx* c)
         if (c->sub[k]) hipStreamDestroy(c->sub[k]);
         if (c->ev_join[k]) hipEventDestroy(c->ev_join[k]);
         if (c->ev_o0[k]) hipEventDestroy(c->ev_o0[k]);
-        c->sub[k] = nullptr; c->ev_join[k] = nullptr; c->ev_o0[k] = nullptr;
+        if (c->ev_small[k]) hipEventDestroy(c->ev_small[k]);
+        c->sub[k] = nullptr; c->ev_join[k] = nullptr; c->ev_o0[k] = nullptr; c->ev_small[k] = nullptr;
     }
     if (c->ev_fork) hipEventDestroy(c->ev_fork);
     c->ev_fork = nullptr;
@@ -271,6 +272,7 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
         if (e != hipSuccess) return bail("stream", e);
         if ((e = hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
         if ((e = hipEventCreateWithFlags(&c->ev_o0[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
+        if ((e = hipEventCreateWithFlags(&c->ev_small[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
     }
     if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("event", e);
     for (int k = 0; k < 2; ++k) {
@@ -644,12 +646,14 @@ static SetRef set_ref(vo_ctx* c, int set)
 #ifndef VO_EXT_SPLIT
 #define VO_EXT_SPLIT 1
 #endif
-// Where the LDS-sized octaves (k_small_pyr: one 1024-thread workgroup per image, ~120 KB of LDS)
-// run: 0 at the scale space's tail, 1 at the head of the feature stream's second part (after
-// ev_join, before the extremum test of octaves 1..), where the previous batch's descriptor
-// waves no longer hold the CUs' LDS.
-#ifndef VO_SMALL_ON_FEATURE
-#define VO_SMALL_ON_FEATURE 0
+// Where the LDS-sized octaves (k_small_pyr: one 1024-thread workgroup per image, ~120 KB of LDS,
+// 0.13 ms isolated but ~1 ms in situ while it waits for a CU with that much free LDS) run:
+// 0 at the scale space's tail; 1 at the head of the feature stream's second part (measured
+// slower: the feature stream is the critical one at 128 frames per step); 2 on a
+// stream of their own (sub[2]) after the level blurs, so neither stream waits for its
+// placement -- only the extremum test of the small octaves does.
+#ifndef VO_SMALL_STREAM
+#define VO_SMALL_STREAM 0
 #endif
 static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uint8_t* d_r, int B, bool join,
                                bool fork = true)
@@ -657,12 +661,14 @@ static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uin
     const size_t fs = (size_t)c->rows * c->cols;
     const int parts = std::min(c->n_sub, B);
     SetRef S = set_ref(c, set);
-    hipStream_t sp = c->sub[0], st = c->sub[1];
+    hipStream_t sp = c->sub[0], st = c->sub[1], ss = c->sub[2];
     if (fork) {                                                 // inputs / earlier work on `stream`
         HIPC(c, hipEventRecord(c->ev_fork, c->stream));
         HIPC(c, hipStreamWaitEvent(sp, c->ev_fork, 0));
     }
     HIPC(c, hipStreamWaitEvent(sp, c->ev_done[set], 0));      // set free (its previous features done)
+    const int o_small = sift_small_octave(c->py);
+    const bool ext_on_st = VO_EXT_SPLIT || VO_SMALL_STREAM != 0;   // the test of octaves 1.. on st
     // scale space on sp; octave 0's extremum test on st as soon as octave 0 is built (beside the
     // scale space of octaves 1..), the other octaves' on st after the scale space (VO_EXT_SPLIT)
     // -- the split that balances the two streams
@@ -671,21 +677,31 @@ static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uin
         ImageSrc src{d_l + f0 * fs, d_r + f0 * fs, fs, c->cols, 0};
         SiftBuffers v = sift_view(*S.sb, c->py, 2 * f0, 2 * nf);
         sift_enqueue_pyramid(c->py, v, src, 2 * nf, c->sp, sp, c->d_py, c->ev_o0[p]);
-        if (!VO_SMALL_ON_FEATURE)
-            sift_enqueue_pyramid_tail(c->py, v, 2 * nf, c->sp, sp, c->d_py, VO_EXT_SPLIT ? c->py.n_oct : 1);
+        if (VO_SMALL_STREAM == 0) sift_enqueue_small(c->py, v, 2 * nf, sp, c->d_py);
+        if (!ext_on_st) sift_enqueue_extrema(c->py, v, 2 * nf, c->sp, sp, c->d_py, 1, c->py.n_oct);
         HIPC(c, hipEventRecord(c->ev_join[p], sp));
+        if (VO_SMALL_STREAM == 2) {
+            HIPC(c, hipStreamWaitEvent(ss, c->ev_join[p], 0));
+            sift_enqueue_small(c->py, v, 2 * nf, ss, c->d_py);
+            HIPC(c, hipEventRecord(c->ev_small[p], ss));
+        }
     }
     for (int p = 0; p < parts; ++p) {
         const int f0 = B * p / parts, nf = B * (p + 1) / parts - f0;
         SiftBuffers v = sift_view(*S.sb, c->py, 2 * f0, 2 * nf);
         // (a synchronous profiled call -- bench.py's isolated pass -- starts it after the whole
         // scale space, so its per-kernel durations stay undisturbed)
-        HIPC(c, hipStreamWaitEvent(st, c->prof.on && join ? c->ev_join[p] : c->ev_o0[p], 0));
+        const bool iso = c->prof.on && join;
+        if (iso && VO_SMALL_STREAM == 2) HIPC(c, hipStreamWaitEvent(st, c->ev_small[p], 0));
+        HIPC(c, hipStreamWaitEvent(st, iso ? c->ev_join[p] : c->ev_o0[p], 0));
         sift_enqueue_extrema(c->py, v, 2 * nf, c->sp, st, c->d_py, 0, 1);
         HIPC(c, hipStreamWaitEvent(st, c->ev_join[p], 0));
-        if (VO_SMALL_ON_FEATURE)
-            sift_enqueue_pyramid_tail(c->py, v, 2 * nf, c->sp, st, c->d_py, VO_EXT_SPLIT ? c->py.n_oct : 1);
-        if (VO_EXT_SPLIT) sift_enqueue_extrema(c->py, v, 2 * nf, c->sp, st, c->d_py, 1, c->py.n_oct);
+        if (VO_SMALL_STREAM == 1) sift_enqueue_small(c->py, v, 2 * nf, st, c->d_py);
+        if (ext_on_st) {
+            sift_enqueue_extrema(c->py, v, 2 * nf, c->sp, st, c->d_py, 1, o_small);
+            if (VO_SMALL_STREAM == 2) HIPC(c, hipStreamWaitEvent(st, c->ev_small[p], 0));
+            sift_enqueue_extrema(c->py, v, 2 * nf, c->sp, st, c->d_py, o_small, c->py.n_oct);
+        }
         sift_enqueue_features(c->py, v, 2 * nf, c->sp, st, c->d_py);
         match_launch(match_view(*S.mb, f0), S.jobs + f0, nf, c->mp, st);
     }

@@ -185,6 +185,9 @@ void sift_enqueue_pyramid_tail(const Pyramid& py, SiftBuffers& b, int n_img, con
                                const Pyramid* d_py, int ext_o_begin);
 void sift_enqueue_extrema(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
                           const Pyramid* d_py, int o_begin, int o_end);
+// the LDS-sized octaves o >= sift_small_octave(py) (one k_small_pyr launch; n_oct when none)
+int sift_small_octave(const Pyramid& py);
+void sift_enqueue_small(const Pyramid& py, SiftBuffers& b, int n_img, hipStream_t s, const Pyramid* d_py);
 void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const vo_sift_params& p, hipStream_t s,
                            const Pyramid* d_py);
 

@@ -20,7 +20,7 @@ if len(sys.argv) > 3 and sys.argv[3] == "street":
     dl, dr = dl.contiguous(), dr.contiguous()
     rows, cols = street.KITTI_ROWS, street.KITTI_COLS
 else:
-    L, R = syn.independent_pairs(B, px_per_cell=syn.BENCH_PX_PER_CELL)
+    L, R = syn.independent_pairs(B, px_per_cell=syn.BENCH_PX_PER_CELL, threads=16)
     dl, dr = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
     rows, cols = 375, 1242
 torch.cuda.synchronize()
