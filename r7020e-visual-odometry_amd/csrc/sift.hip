@@ -868,8 +868,12 @@ __global__ __launch_bounds__(256) void k_down(const float* __restrict__ src, siz
 // pass, acc = k0*s0; acc = fmaf(kj, s[-j] + s[+j], acc)); reflect-101 indices
 // come from per-octave LDS tables.
 // ---------------------------------------------------------------------------
-#define VO_SMALL_PX 9216          // 3 planes + the next base fit in 160 KB of LDS
+#ifndef VO_SMALL_PX
+#define VO_SMALL_PX 9216          // largest plane of the LDS path: 3 planes + the next base fit in 160 KB
+#endif
+#ifndef VO_SMALL_T
 #define VO_SMALL_T 1024
+#endif
 
 // Register-blocked passes of k_small_pyr: one thread computes SMV consecutive outputs along the
 // filter direction from the SMV + 2r inputs it reads once (reflect-101 through the tables only
@@ -916,16 +920,16 @@ __device__ __forceinline__ void small_pass(const float* __restrict__ src, float*
 }
 
 __global__ __launch_bounds__(VO_SMALL_T) void k_small_pyr(const Pyramid* __restrict__ py, float* __restrict__ arena,
-                                                          int o_first, int rtab)
+                                                          int o_first, int rtab, int cap, int bcap)
 {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int img = blockIdx.x, tid = threadIdx.x;
     const int L = py->L, NL = L + 3;
-    float* cur = sm;                                  // G_{i-1}
-    float* tmp = sm + VO_SMALL_PX;                    // row-pass output
-    float* nxt = sm + 2 * VO_SMALL_PX;                // G_i
-    float* base = sm + 3 * VO_SMALL_PX;               // next octave's G_0 (<= VO_SMALL_PX / 4)
-    int* ridx = reinterpret_cast<int*>(base + VO_SMALL_PX / 4);       // reflect-101 tables
+    float* cur = sm;                                  // G_{i-1}   (cap = the largest plane, a multiple of 4)
+    float* tmp = sm + cap;                            // row-pass output
+    float* nxt = sm + 2 * cap;                        // G_i
+    float* base = sm + 3 * cap;                       // next octave's G_0 (bcap = the largest such plane)
+    int* ridx = reinterpret_cast<int*>(base + bcap);                  // reflect-101 tables
     int* cidx = ridx + rtab;                          // rtab >= rows + 2r of every octave here
     for (int o = o_first; o < py->n_oct; ++o) {
         const OctGeom& g = py->oct[o];
@@ -2226,23 +2230,30 @@ static int fused_octaves(const Pyramid& py)
 
 // First octave from which every remaining octave fits the one-launch LDS path (k_small_pyr),
 // its reflect-table length and dynamic LDS size.
-struct SmallPlan { int o_small, rtab; size_t lds; };
+// LDS holds 3 planes of the largest octave (cap floats), the largest next-octave base (bcap
+// floats; both rounded up to a multiple of 4) and the reflect tables -- sized to the octaves at
+// hand, not to VO_SMALL_PX, so a launch needs no more of a CU's LDS than its planes.
+struct SmallPlan { int o_small, rtab, cap, bcap; size_t lds; };
 static SmallPlan small_plan(const Pyramid& py)
 {
-    SmallPlan sp{py.n_oct, 0, 0};
+    SmallPlan sp{py.n_oct, 0, 0, 0, 0};
     int maxr = 0;
     for (int i = 1; i < py.L + 3; ++i) maxr = std::max(maxr, py.krad[i]);
     for (int o = py.n_oct - 1; o >= 1; --o) {
-        int rt = 0, ct = 0;
+        int rt = 0, ct = 0, cap = 0, bcap = 0;
         bool fits = true;
         for (int q = o; q < py.n_oct; ++q) {
             fits = fits && py.oct[q].rows * py.oct[q].cols <= VO_SMALL_PX;
+            cap = std::max(cap, py.oct[q].rows * py.oct[q].cols);
+            if (q > o) bcap = std::max(bcap, py.oct[q].rows * py.oct[q].cols);
             rt = std::max(rt, py.oct[q].rows + 2 * maxr);
             ct = std::max(ct, py.oct[q].cols + 2 * maxr);
         }
-        const size_t lds = sizeof(float) * (3 * VO_SMALL_PX + VO_SMALL_PX / 4) + sizeof(int) * (rt + ct);
+        cap = (cap + 3) & ~3;
+        bcap = (bcap + 3) & ~3;
+        const size_t lds = sizeof(float) * (3 * (size_t)cap + bcap) + sizeof(int) * (rt + ct);
         if (!fits || lds > 160 * 1024) break;
-        sp = SmallPlan{o, rt, lds};
+        sp = SmallPlan{o, rt, cap, bcap, lds};
     }
     return sp;
 }
@@ -2260,7 +2271,7 @@ void sift_enqueue_small(const Pyramid& py, SiftBuffers& b, int n_img, hipStream_
 
     raise_lds_limit((const void*)k_small_pyr);
     VO_LAUNCH_NAMED("k_blur_small", k_small_pyr, dim3(n_img), dim3(VO_SMALL_T), sp.lds, s, d_py, b.arena, sp.o_small,
-                    sp.rtab);
+                    sp.rtab, sp.cap, sp.bcap);
 }
 
 void sift_enqueue_pyramid(const Pyramid& py, SiftBuffers& b, const ImageSrc& src, int n_img, const vo_sift_params& p,
