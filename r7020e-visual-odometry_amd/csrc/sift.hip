@@ -1177,6 +1177,149 @@ __global__ __launch_bounds__(64) void k_ext_stream(const Pyramid* __restrict__ p
 #undef VO_ET_LOAD
 }
 
+// The inner part of the extremum test (VO_EXT_INNER, the default): the same streaming wave with
+// only G_1 .. G_{L+1} loaded -- D_1 .. D_L, the centres of every layer and every neighbour level
+// except D_0 (layer 1's lower neighbour, G_1 - G_0) and D_{L+1} (layer L's upper one).  A bit is
+// set when its centre passes |val| > thr and the extremum test against those streamed levels;
+// k_refine completes the test for layers 1 and L (val >= / <= the 9 values of D_0 / D_{L+1})
+// before anything else and rejects the centres that fail it.  val >= max of the 27 <=> val >=
+// the max of each part, so the keypoints are the full test's; 2 of the L + 3 planes leave the
+// streamed bytes (4 (L + 1) B per octave px).  Measured: the extremum test 3.28 -> 2.34 ms, k_refine
+// 0.39 -> 0.77 ms isolated (the partial candidates), +3.5-3.9 % stereo frames/s.
+template <int L>
+__global__ __launch_bounds__(64) void k_ext_inner(const Pyramid* __restrict__ py, const float* __restrict__ arena,
+                                                   unsigned long long* __restrict__ mask, float thr, int n_img, int u_first,
+                                                   int u_last)
+{
+    vo_ss_prio();
+    constexpr int NG = L + 1, ND = L, W = 3;          // streamed levels G_1..G_{L+1}, DoG D_1..D_L
+    const int lane = threadIdx.x;
+    const int u_all = xcd_remap(blockIdx.x, gridDim.x);
+    const int nu = u_last - u_first;
+    const int img = u_all / nu;
+    int u = u_first + u_all - img * nu;
+    int o = 0;
+    while (o + 1 < py->n_oct && py->ebase[o + 1] <= u) ++o;
+    o = __builtin_amdgcn_readfirstlane(o);
+    u -= py->ebase[o];
+    const OctGeom& g = py->oct[o];
+    const int rows = g.rows, cols = g.cols, pitch = g.pitch;
+    const int ns = py->estrips[o];
+    const int strip = u % ns, band = u / ns;
+    const int ir = rows - 2 * VO_SIFT_BORDER;
+    const int r0 = VO_SIFT_BORDER + band * VO_EXT_BAND;
+    const int nrow = min(VO_EXT_BAND, ir - band * VO_EXT_BAND);
+    const int xs = strip * 128, xa = xs + 2 * lane, xb = xa + 1;
+    const int hx = lane == 63 ? xs + 128 : max(xs - 1, 0);
+    const float* base = arena + img * py->istride;
+    size_t goff[NG];
+#pragma unroll
+    for (int lv = 0; lv < NG; ++lv) goff[lv] = g.g_off[lv + 1];
+    const int wr = py->wrow[o];
+    unsigned long long* mrow = mask + (size_t)img * py->n_words;
+#if VO_EXT_BSTORE
+    const __amdgpu_buffer_rsrc_t rs_m = __builtin_amdgcn_make_buffer_rsrc(mrow, 0, py->n_words * 8, 0x00020000);
+#endif
+    int wb[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) wb[l] = py->wbase[o * L + l];
+    const bool in0 = xa >= VO_SIFT_BORDER && xa < cols - VO_SIFT_BORDER;
+    const bool in1 = xb >= VO_SIFT_BORDER && xb < cols - VO_SIFT_BORDER;
+
+    typedef float f2_t __attribute__((ext_vector_type(2)));
+    f2_t pm[W][NG];
+    float ph[W][NG];
+    f2_t hmx[W][ND], hmn[W][ND];
+    f2_t dc[W][L];
+
+#define VO_ES_LOAD(T, SL)                                                                          \
+    do {                                                                                           \
+        const int y_ = min(r0 - 1 + (T), rows - 1);                                                \
+        const float* rp_ = base + (size_t)y_ * pitch;                                              \
+        _Pragma("unroll") for (int lv = 0; lv < NG; ++lv) {                                        \
+            if (xa < cols) pm[SL][lv] = *reinterpret_cast<const f2_t*>(rp_ + goff[lv] + xa);      \
+            ph[SL][lv] = rp_[goff[lv] + hx];                                                       \
+        }                                                                                          \
+    } while (0)
+
+    auto step = [&](int t, auto sl_c, auto test_c) {
+        constexpr int SL = decltype(sl_c)::value;
+        f2_t d[ND];
+        float hd[ND];
+#pragma unroll
+        for (int lv = 0; lv < ND; ++lv) {
+            d[lv] = pm[SL][lv + 1] - pm[SL][lv];
+            hd[lv] = ph[SL][lv + 1] - ph[SL][lv];
+        }
+        if (t + W <= nrow + 1) VO_ES_LOAD(t + W, SL);
+#pragma unroll
+        for (int lv = 0; lv < ND; ++lv) {
+            const float la = vo_wave_shr1_or(hd[lv], d[lv].y), rb = vo_wave_shl1_or(hd[lv], d[lv].x);
+            hmx[SL][lv] = f2_t{fmaxf(fmaxf(la, d[lv].x), d[lv].y), fmaxf(fmaxf(d[lv].x, d[lv].y), rb)};
+            hmn[SL][lv] = f2_t{fminf(fminf(la, d[lv].x), d[lv].y), fminf(fminf(d[lv].x, d[lv].y), rb)};
+        }
+#pragma unroll
+        for (int l = 0; l < L; ++l) dc[SL][l] = d[l];
+        if constexpr (decltype(test_c)::value) {
+            constexpr int A = (SL + 1) % W, M = (SL + 2) % W;
+            const int r = r0 + t - 2;
+            const bool live = t - 2 < nrow;
+            f2_t mx3[ND], mn3[ND];
+#pragma unroll
+            for (int lv = 0; lv < ND; ++lv) {
+                mx3[lv] = f2_t{fmaxf(fmaxf(hmx[A][lv].x, hmx[M][lv].x), hmx[SL][lv].x),
+                               fmaxf(fmaxf(hmx[A][lv].y, hmx[M][lv].y), hmx[SL][lv].y)};
+                mn3[lv] = f2_t{fminf(fminf(hmn[A][lv].x, hmn[M][lv].x), hmn[SL][lv].x),
+                               fminf(fminf(hmn[A][lv].y, hmn[M][lv].y), hmn[SL][lv].y)};
+            }
+#pragma unroll
+            for (int layer = 1; layer <= L; ++layer) {
+                // streamed DoG D_k sits at index k - 1: D_layer always, D_{layer-1} if layer >= 2,
+                // D_{layer+1} if layer <= L - 1
+                bool pos[2], neg[2];
+                float val[2];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    val[c] = c ? dc[M][layer - 1].y : dc[M][layer - 1].x;
+                    float bmx = c ? mx3[layer - 1].y : mx3[layer - 1].x;
+                    float bmn = c ? mn3[layer - 1].y : mn3[layer - 1].x;
+                    if (layer >= 2) {
+                        bmx = fmaxf(bmx, c ? mx3[layer - 2].y : mx3[layer - 2].x);
+                        bmn = fminf(bmn, c ? mn3[layer - 2].y : mn3[layer - 2].x);
+                    }
+                    if (layer <= L - 1) {
+                        bmx = fmaxf(bmx, c ? mx3[layer].y : mx3[layer].x);
+                        bmn = fminf(bmn, c ? mn3[layer].y : mn3[layer].x);
+                    }
+                    pos[c] = (val[c] > thr) & (val[c] >= bmx);
+                    neg[c] = (val[c] < -thr) & (val[c] <= bmn);
+                }
+                const uint64_t w0 = __ballot((pos[0] | neg[0]) & in0), w1 = __ballot((pos[1] | neg[1]) & in1);
+                const int k = 2 * strip + lane;
+#if VO_EXT_BSTORE
+                const uint32_t mo = (lane < 2 && live) ? (uint32_t)(wb[layer - 1] + (r - VO_SIFT_BORDER) * wr + k) * 8u
+                                                       : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(vo_i2, (uint64_t)(lane ? w1 : w0)), rs_m, mo, 0, 0);
+#else
+                if (lane < 2 && live)
+                    mrow[wb[layer - 1] + (size_t)(r - VO_SIFT_BORDER) * wr + k] = lane ? w1 : w0;
+#endif
+            }
+        }
+    };
+
+    vo_static_for<W>([&](auto c) { VO_ES_LOAD(decltype(c)::value, decltype(c)::value); });
+    step(0, std::integral_constant<int, 0>{}, std::false_type{});
+    step(1, std::integral_constant<int, 1>{}, std::false_type{});
+#pragma unroll 1
+    for (int t0 = 2; t0 < nrow + 2; t0 += W) {
+        step(t0, std::integral_constant<int, 2>{}, std::true_type{});
+        step(t0 + 1, std::integral_constant<int, 0>{}, std::true_type{});
+        step(t0 + 2, std::integral_constant<int, 1>{}, std::true_type{});
+    }
+#undef VO_ES_LOAD
+}
+
 // Block-wide exclusive scan of one value per thread (1024 threads).
 __device__ __forceinline__ uint32_t block_exscan_1024(uint32_t v, uint32_t* sh, uint32_t* total)
 {
@@ -1477,6 +1620,30 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
         float xi = 0, xr = 0, xc = 0;
         int it = 0;
         bool ok = true;
+#if VO_EXT_INNER
+        // the extremum test's remaining part (k_ext_inner streams G_1 .. G_{L+1} only): a centre of
+        // layer 1 / L must also be >= (val > 0) or <= (val < 0) the 9 values of D_0 / D_{L+1}
+        // around it.  It passed the rest of the 26-neighbour test with |val| > thr, so this is
+        // the dense kernel's mask bit exactly; a candidate that fails is rejected here.
+        if (layer0 == 1 || layer0 == L) {
+            const float* gb = arena + img * py->istride;
+            const float v = DOGV(gb + g.g_off[layer0], P, r0, c0);
+            float mx = -INFINITY, mn = INFINITY;
+            auto outer = [&](const float* pl) {
+#pragma unroll
+                for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                    for (int dx = -1; dx <= 1; ++dx) {
+                        const float d = DOGV(pl, P, r0 + dy, c0 + dx);
+                        mx = fmaxf(mx, d); mn = fminf(mn, d);
+                    }
+            };
+            if (layer0 == 1) outer(gb + g.g_off[0]);
+            if (layer0 == L) outer(gb + g.g_off[L + 1]);
+            ok = v > 0.0f ? v >= mx : v <= mn;
+        }
+        if (ok)
+#endif
         for (; it < VO_SIFT_MAX_INTERP; ++it) {
             const float* gb = arena + img * py->istride;
             const float* im = gb + g.g_off[layer];          // DoG level l = G_{l+1} - G_l (VO_DOG)
@@ -2369,13 +2536,19 @@ void sift_enqueue_extrema(const Pyramid& py, SiftBuffers& b, int n_img, const vo
     const int u_first = py.ebase[std::max(o_begin, fused_octaves(py))], u_last = py.ebase[o_end];
     if (u_last > u_first) {
         const dim3 ge((u_last - u_first) * n_img);
+#if VO_EXT_INNER
+#define VO_EXT_K(LL) VO_LAUNCH(k_ext_inner<LL>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first, u_last)
+#else
+#define VO_EXT_K(LL) VO_LAUNCH(k_ext_stream<LL>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first, u_last)
+#endif
         switch (L) {
-        case 1: VO_LAUNCH(k_ext_stream<1>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first, u_last); break;
-        case 2: VO_LAUNCH(k_ext_stream<2>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first, u_last); break;
-        case 3: VO_LAUNCH(k_ext_stream<3>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first, u_last); break;
-        case 4: VO_LAUNCH(k_ext_stream<4>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first, u_last); break;
-        default: VO_LAUNCH(k_ext_stream<5>, ge, dim3(64), 0, s, d_py, A, b.mask, thr, n_img, u_first, u_last); break;
+        case 1: VO_EXT_K(1); break;
+        case 2: VO_EXT_K(2); break;
+        case 3: VO_EXT_K(3); break;
+        case 4: VO_EXT_K(4); break;
+        default: VO_EXT_K(5); break;
         }
+#undef VO_EXT_K
     }
 }
 

@@ -101,6 +101,9 @@ static inline __host__ __device__ int dt_stride(int dcap) { return (DT_HDR + 3 *
 #ifndef VO_EXT_BAND
 #define VO_EXT_BAND 30            // interior rows per extremum-test wave (a multiple of 3)
 #endif
+#ifndef VO_EXT_INNER
+#define VO_EXT_INNER 1            // extremum test: 1 = k_ext_inner + k_refine's outer-level check, 0 = k_ext_stream (all L+3 levels)
+#endif
 #ifndef VO_EXT_BSTORE
 #define VO_EXT_BSTORE 1           // extremum test: mask words by unconditional buffer stores (0: branchy stores)
 #endif

@@ -53,9 +53,11 @@ def fused_octaves(rows: int, cols: int, layers: int = 3, enabled: bool = False) 
     return n
 
 
-def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3, fused: bool = False) -> dict:
+def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3, fused: bool = False, ext_inner: bool = True) -> dict:
     """Algorithmic bytes per CALL (all launches of that kernel name in one
-    batch of n_img images) and launches per call, per kernel name."""
+    batch of n_img images) and launches per call, per kernel name.  ext_inner: the
+    extremum test as k_ext_inner (the default build, VO_EXT_INNER=1: G_1..G_{L+1} streamed,
+    the outer levels checked by k_refine around candidates) instead of k_ext_stream (all L+3)."""
     dims = octave_dims(rows, cols)
     lv = layers + 2          # blurred levels per octave (1..L+2)
     n_fused = fused_octaves(rows, cols, layers, fused)
@@ -83,10 +85,12 @@ def kernel_bytes(rows: int, cols: int, n_img: int, layers: int = 3, fused: bool 
             continue
         nb = 4 * dims[o + 1][0] * dims[o + 1][1] * n_img if o + 1 < o_small else 0
         add("k_blur_fused", 8 * px * lv + nb, lv)                         # G_{i-1} in, G_i out (+ next base)
-    # extremum test reads the L+3 Gaussian levels of every other octave once (DoG formed on chip)
+    # extremum test reads the L+1 (k_ext_inner) or L+3 (k_ext_stream) Gaussian levels of every
+    # octave once (DoG formed on chip)
     # two launches when octave 0 is tested separately (on the feature stream, beside the scale
     # space of octaves 1..; the rest at the scale space's tail)
-    ext = sum(4 * (layers + 3) * r * c for o, (r, c) in enumerate(dims) if o >= n_fused) * n_img
+    nlev = layers + 1 if ext_inner else layers + 3
+    ext = sum(4 * nlev * r * c for o, (r, c) in enumerate(dims) if o >= n_fused) * n_img
     if ext:
-        add(f"k_ext_stream<{layers}>", ext, 2 if n_fused == 0 and len(dims) > 1 else 1)
+        add(f"k_ext_{'inner' if ext_inner else 'stream'}<{layers}>", ext, 2 if n_fused == 0 and len(dims) > 1 else 1)
     return out

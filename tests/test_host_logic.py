@@ -39,7 +39,9 @@ def test_roofline_model_matches_survey():
     assert kb["k_blur_fused"][1] == 4 * 5 and "k_down" not in kb and kb["k_blur_small"][1] == 1
     assert kb["k_blur_fused"][0] == 2 * sum(8 * 5 * r * c + (4 * dims[o + 1][0] * dims[o + 1][1] if o < 3 else 0)
                                             for o, (r, c) in enumerate(dims[:4]))
-    assert kb["k_ext_stream<3>"][0] == 2 * sum(4 * 6 * r * c for r, c in dims)
+    assert kb["k_ext_inner<3>"][0] == 2 * sum(4 * 4 * r * c for r, c in dims)      # G_1..G_4 streamed
+    kd = roofline.kernel_bytes(375, 1242, 2, fused=False, ext_inner=False)
+    assert kd["k_ext_stream<3>"][0] == 2 * sum(4 * 6 * r * c for r, c in dims)     # all L+3 levels
     # experimental k_octave path (test build libvo_exp.so, vo_exp_set): octaves 0..3 (>= 256 columns, >= 64 rows)
     # are one launch each (levels, extremum test, next base)
     kf = roofline.kernel_bytes(375, 1242, 2, fused=True)

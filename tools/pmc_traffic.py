@@ -24,6 +24,7 @@ RULES = [
     (r"k_small_pyr", "k_blur_small"),
     (r"k_base_src<true>", "k_base_src<true>"),
     (r"k_ext_stream<(\d)>", r"k_ext_stream<\1>"),
+    (r"k_ext_inner<(\d)>", r"k_ext_inner<\1>"),
     (r"vo::(k_\w+)", r"\1"),
 ]
 
