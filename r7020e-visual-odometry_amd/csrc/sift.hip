@@ -1628,19 +1628,25 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
         if (layer0 == 1 || layer0 == L) {
             const float* gb = arena + img * py->istride;
             const float v = DOGV(gb + g.g_off[layer0], P, r0, c0);
-            float mx = -INFINITY, mn = INFINITY;
-            auto outer = [&](const float* pl) {
+            // v >= the max of the 9 <=> v >= each: the value straight below / above first (2 loads;
+            // most partial candidates that fail, fail there), the other 8 only if it passes
+            auto beats = [&](float d) { return v > 0.0f ? v >= d : v <= d; };
+            if (layer0 == 1) ok = beats(DOGV(gb + g.g_off[0], P, r0, c0));
+            if (layer0 == L) ok = ok && beats(DOGV(gb + g.g_off[L + 1], P, r0, c0));
+            if (ok) {
+                float mx = -INFINITY, mn = INFINITY;
+                auto ring = [&](const float* pl) {
 #pragma unroll
-                for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-                    for (int dx = -1; dx <= 1; ++dx) {
-                        const float d = DOGV(pl, P, r0 + dy, c0 + dx);
+                    for (int q = 0; q < 9; ++q) {
+                        if (q == 4) continue;
+                        const float d = DOGV(pl, P, r0 + q / 3 - 1, c0 + q % 3 - 1);
                         mx = fmaxf(mx, d); mn = fminf(mn, d);
                     }
-            };
-            if (layer0 == 1) outer(gb + g.g_off[0]);
-            if (layer0 == L) outer(gb + g.g_off[L + 1]);
-            ok = v > 0.0f ? v >= mx : v <= mn;
+                };
+                if (layer0 == 1) ring(gb + g.g_off[0]);
+                if (layer0 == L) ring(gb + g.g_off[L + 1]);
+                ok = v > 0.0f ? v >= mx : v <= mn;
+            }
         }
         if (ok)
 #endif
