@@ -45,7 +45,15 @@ I8_MFMA_PEAK_TOPS = 5000.0     # MI355X_MICROARCH.md "Matrix cores": I8 = 2x the
 # per-launch HBM bytes of each kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes on this
 # workload (tools/pmc_passes.sh + tools/pmc_traffic.py; FETCH_SIZE doubled on gfx950)
 # (the newest profiles/r<NN>_pmc_traffic.json)
-TRAFFIC_FILE = max(ROOT.glob("profiles/r*_pmc_traffic.json"), default=ROOT / "profiles" / "r01_pmc_traffic.json")
+def _traffic_key(p):
+    # r<NN>_<tag>_pmc_traffic.json: the round, then the tag in a..z, aa..zz order
+    parts = p.name.split("_")
+    tag = parts[1] if len(parts) > 3 else ""
+    return (int(parts[0][1:]) if parts[0][1:].isdigit() else 0, len(tag), tag)
+
+
+TRAFFIC_FILE = max(ROOT.glob("profiles/r*_pmc_traffic.json"), key=_traffic_key,
+                   default=ROOT / "profiles" / "r01_pmc_traffic.json")
 
 
 def parse():
