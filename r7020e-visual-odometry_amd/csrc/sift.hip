@@ -1598,6 +1598,7 @@ __device__ __forceinline__ void solve3_dev(const float H[9], const float b[3], f
 __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                                 const uint32_t* __restrict__ cand, const int* __restrict__ n_cand,
                                                 CandOut* __restrict__ cout, int* __restrict__ acc, int* __restrict__ n_acc,
+                                                uint32_t* __restrict__ knpk,
                                                 int cand_cap, int n_img, float contrast_thr, float edge_thr, float sigma)
 {
     const int L = py->L;
@@ -1703,6 +1704,9 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
         out->xo = xo; out->yo = yo; out->scl = scl; out->response = resp;
         out->o = o; out->layer = layer; out->r = r; out->c = c;
         out->npk = ok ? -1 : 0;
+#if VO_NPK_COMPACT
+        knpk[(size_t)img * cand_cap + kidx] = ok ? 0xFFFFFFFFu : 0u;   // k_orient writes the accepted ones' count
+#endif
         // the accepted candidates as a list (k_orient walks only those: on KITTI-00 street frames
         // ~6 in 7 candidates are rejected here, profiles/r05_d_content_pmc_*); the list order is
         // free -- every result is stored at its candidate's index
@@ -1757,7 +1761,7 @@ __device__ __forceinline__ uint32_t desc_fxq(float v)
 template <int HS>
 __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                                const int* __restrict__ n_acc, const int* __restrict__ acc,
-                                               CandOut* __restrict__ cout, int cand_cap, int n_img)
+                                               CandOut* __restrict__ cout, uint32_t* __restrict__ knpk, int cand_cap, int n_img)
 {
     // HS: bins per lane column (>= 36).  Layout hp[bin * 64 + lane].
     constexpr int NC = VO_ORIENT_COLS;             // histogram columns: lane l adds into column l % NC
@@ -1878,7 +1882,12 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
             out->ang[rank] = ang;
         }
         __syncthreads();
-        if (lane == 0) out->npk = __popcll(bal);
+        if (lane == 0) {
+            out->npk = __popcll(bal);
+#if VO_NPK_COMPACT
+            knpk[(size_t)img * cand_cap + kidx] = (uint32_t)__popcll(bal);
+#endif
+        }
     }
 }
 
@@ -1895,10 +1904,20 @@ __global__ __launch_bounds__(1024) void k_scan_cands(const CandOut* __restrict__
     const int chunk = (n + 1023) / 1024;
     const int a = tid * chunk, e = min(a + chunk, n);
     uint32_t s = 0;
+#if VO_NPK_COMPACT
+    // the peak counts as k_refine / k_orient left them in koff (4 B per candidate instead of a
+    // CandOut line each), scanned in place
+    (void)co;
+    for (int k = a; k < e; ++k) s += ko[k];
+    uint32_t total;
+    uint32_t base = block_exscan_1024(s, sh, &total);
+    for (int k = a; k < e; ++k) { const uint32_t v = ko[k]; ko[k] = base; base += v; }
+#else
     for (int k = a; k < e; ++k) s += (uint32_t)co[k].npk;
     uint32_t total;
     uint32_t base = block_exscan_1024(s, sh, &total);
     for (int k = a; k < e; ++k) { ko[k] = base; base += (uint32_t)co[k].npk; }
+#endif
     if (tid == 0) n_kp[img] = (int)total;
 }
 
@@ -2597,12 +2616,12 @@ void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const v
     VO_LAUNCH(k_seg_count, gs, dim3(256), 0, s, b.mask, b.woff, py.n_words, py.n_seg);
     VO_LAUNCH(k_seg_scan, dim3(n_img), dim3(1024), 0, s, b.woff, b.n_cand, b.n_acc, py.n_seg);
     VO_LAUNCH(k_seg_emit, gs, dim3(256), 0, s, d_py, b.mask, (const uint32_t*)b.woff, b.cand, b.cand_cap);
-    VO_LAUNCH(k_refine, dim3(VO_REFINE_BLOCKS), dim3(256), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.acc, b.n_acc, b.cand_cap, n_img,
+    VO_LAUNCH(k_refine, dim3(VO_REFINE_BLOCKS), dim3(256), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.acc, b.n_acc, b.koff, b.cand_cap, n_img,
               p.contrast_threshold, p.edge_threshold, p.sigma);
     const size_t fpre_bytes = sizeof(int) * (size_t)(n_img + 1);
     const int* n_walk = VO_ACC_LIST ? b.n_acc : b.n_cand;    // the accepted list, or every candidate
     VO_LAUNCH_NAMED("k_orient", (k_orient<36>), dim3(kFeatureGrid), dim3(64), fpre_bytes, s, d_py, A, n_walk, b.acc,
-                    b.cout, b.cand_cap, n_img);
+                    b.cout, b.koff, b.cand_cap, n_img);
     VO_LAUNCH(k_scan_cands, dim3(n_img), dim3(1024), 0, s, b.cout, b.n_cand, b.koff, b.n_kp, b.cand_cap);
     VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, n_walk, b.acc, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
                        n_img, p.upsample);

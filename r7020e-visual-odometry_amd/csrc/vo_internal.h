@@ -104,6 +104,9 @@ static inline __host__ __device__ int dt_stride(int dcap) { return (DT_HDR + 3 *
 #ifndef VO_EXT_INNER
 #define VO_EXT_INNER 1            // extremum test: 1 = k_ext_inner + k_refine's outer-level check, 0 = k_ext_stream (all L+3 levels)
 #endif
+#ifndef VO_NPK_COMPACT
+#define VO_NPK_COMPACT 1          // peak counts also as a 4-B array (koff, scanned in place) for k_scan_cands
+#endif
 #ifndef VO_EXT_BSTORE
 #define VO_EXT_BSTORE 1           // extremum test: mask words by unconditional buffer stores (0: branchy stores)
 #endif
