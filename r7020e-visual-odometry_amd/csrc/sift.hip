@@ -1621,6 +1621,10 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
         float xi = 0, xr = 0, xc = 0;
         int it = 0;
         bool ok = true;
+        // the last step's terms at its (r, c, layer): the contrast / edge tests below need exactly
+        // these (the loop only exits with ok at convergence, without moving), so they are kept
+        // instead of re-read
+        float kD[3] = {0, 0, 0}, kv = 0, kxx = 0, kyy = 0, kxy = 0;
 #if VO_EXT_INNER
         // the extremum test's remaining part (k_ext_inner streams G_1 .. G_{L+1} only): a centre of
         // layer 1 / L must also be >= (val > 0) or <= (val < 0) the 9 values of D_0 / D_{L+1}
@@ -1654,12 +1658,15 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
         for (; it < VO_SIFT_MAX_INTERP; ++it) {
             const float* gb = arena + img * py->istride;
             const float* im = gb + g.g_off[layer];          // DoG level l = G_{l+1} - G_l (VO_DOG)
-            const float* pv = gb + g.g_off[layer - 1];
-            const float* nx = gb + g.g_off[layer + 1];
+            // the neighbour levels as +-lstride from im (the planes of an octave are lstride
+            // apart), so the loads DOGV(pv) / DOGV(nx) share with DOGV(im) are one load each
+            const float* pv = im - lstride;
+            const float* nx = im + lstride;
             float dD[3] = {(DOGV(im, P, r, c + 1) - DOGV(im, P, r, c - 1)) * ds,
                            (DOGV(im, P, r + 1, c) - DOGV(im, P, r - 1, c)) * ds,
                            (DOGV(nx, P, r, c) - DOGV(pv, P, r, c)) * ds};
-            float v2 = DOGV(im, P, r, c) * 2.0f;
+            const float vc = DOGV(im, P, r, c);
+            float v2 = vc * 2.0f;
             float dxx = (DOGV(im, P, r, c + 1) + DOGV(im, P, r, c - 1) - v2) * ss;
             float dyy = (DOGV(im, P, r + 1, c) + DOGV(im, P, r - 1, c) - v2) * ss;
             float dss = (DOGV(nx, P, r, c) + DOGV(pv, P, r, c) - v2) * ss;
@@ -1667,6 +1674,7 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
             float dxs = (DOGV(nx, P, r, c + 1) - DOGV(nx, P, r, c - 1) - DOGV(pv, P, r, c + 1) + DOGV(pv, P, r, c - 1)) * cs;
             float dys = (DOGV(nx, P, r + 1, c) - DOGV(nx, P, r - 1, c) - DOGV(pv, P, r + 1, c) + DOGV(pv, P, r - 1, c)) * cs;
             float H[9] = {dxx, dxy, dxs, dxy, dyy, dys, dxs, dys, dss};
+            kD[0] = dD[0]; kD[1] = dD[1]; kD[2] = dD[2]; kv = vc; kxx = dxx; kyy = dyy; kxy = dxy;
             float X[3];
             solve3_dev(H, dD, X);
             xi = -X[2]; xr = -X[1]; xc = -X[0];
@@ -1680,20 +1688,10 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
         if (it >= VO_SIFT_MAX_INTERP) ok = false;
         float xo = 0, yo = 0, scl = 0, resp = 0;
         if (ok) {
-            const float* gb = arena + img * py->istride;
-            const float* im = gb + g.g_off[layer];          // DoG level l = G_{l+1} - G_l (VO_DOG)
-            const float* pv = gb + g.g_off[layer - 1];
-            const float* nx = gb + g.g_off[layer + 1];
-            float dD[3] = {(DOGV(im, P, r, c + 1) - DOGV(im, P, r, c - 1)) * ds,
-                           (DOGV(im, P, r + 1, c) - DOGV(im, P, r - 1, c)) * ds,
-                           (DOGV(nx, P, r, c) - DOGV(pv, P, r, c)) * ds};
-            float tt = dD[0] * xc + dD[1] * xr + dD[2] * xi;
-            float contr = DOGV(im, P, r, c) * img_scale + tt * 0.5f;
+            float tt = kD[0] * xc + kD[1] * xr + kD[2] * xi;
+            float contr = kv * img_scale + tt * 0.5f;
             if (fabsf(contr) * (float)L < contrast_thr) ok = false;
-            float v2 = DOGV(im, P, r, c) * 2.0f;
-            float dxx = (DOGV(im, P, r, c + 1) + DOGV(im, P, r, c - 1) - v2) * ss;
-            float dyy = (DOGV(im, P, r + 1, c) + DOGV(im, P, r - 1, c) - v2) * ss;
-            float dxy = (DOGV(im, P, r + 1, c + 1) - DOGV(im, P, r + 1, c - 1) - DOGV(im, P, r - 1, c + 1) + DOGV(im, P, r - 1, c - 1)) * cs;
+            const float dxx = kxx, dyy = kyy, dxy = kxy;
             float tr = dxx + dyy, det = dxx * dyy - dxy * dxy;
             if (det <= 0 || tr * tr * edge_thr >= (edge_thr + 1) * (edge_thr + 1) * det) ok = false;
             xo = (float)c + xc;
