@@ -71,6 +71,7 @@ extern "C" {
 #define VO_ERR_STATE          -6
 
 #define VO_DESC_LEN 128
+#define VO_MAX_BATCH 512         /* largest max_batch of vo_create */
 
 /* detectSIFTFeatures / extractFeatures defaults (MATLAB R2022b+).
  * contrast_threshold is in OpenCV units: MATLAB's ContrastThreshold 0.0133
@@ -124,7 +125,7 @@ void vo_default_match_params(vo_match_params* p);
 void vo_default_ransac_params(vo_ransac_params* p);
 
 /* Create a context on HIP device `device` for images of rows x cols, able to
- * process up to max_batch (1..128) stereo frames per call.  calib may be NULL (then
+ * process up to max_batch (1..VO_MAX_BATCH) stereo frames per call.  calib may be NULL (then
  * vo_step/vo_landmarks are unavailable until vo_set_calib). Returns NULL on
  * failure (message via vo_last_error(NULL)). */
 vo_ctx* vo_create(int device, int rows, int cols, int max_batch,

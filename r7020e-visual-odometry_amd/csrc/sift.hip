@@ -1499,7 +1499,7 @@ __device__ __forceinline__ int wave_incl_scan(int x)
     return x;
 }
 
-#define VO_FLAT_MAX_IMG 258     // 2 * max_batch(128) + 2 image slots
+#define VO_FLAT_MAX_IMG (2 * VO_MAX_BATCH + 2)   // 2 * max_batch + 2 image slots
 __device__ __forceinline__ long flat_setup(const int* __restrict__ counts, int cap, int n_img, int* pre)
 {
     const int tid = threadIdx.x, nt = blockDim.x;

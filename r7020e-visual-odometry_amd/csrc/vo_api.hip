@@ -233,7 +233,7 @@ static void destroy_buffers(vo_ctx* c)
 vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib* calib, const vo_sift_params* sift,
                   const vo_match_params* match, const vo_ransac_params* ransac)
 {
-    if (rows < 16 || cols < 16 || rows > 2048 || cols > 2048 || max_batch < 1 || max_batch > 128) {
+    if (rows < 16 || cols < 16 || rows > 2048 || cols > 2048 || max_batch < 1 || max_batch > VO_MAX_BATCH) {
         fail(nullptr, VO_ERR_ARG, "vo_create: bad size rows=%d cols=%d max_batch=%d", rows, cols, max_batch);
         return nullptr;
     }

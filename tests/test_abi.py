@@ -82,9 +82,9 @@ def test_missing_library_raises(vo, tmp_path):
         vo.load_library(tmp_path / "nope.so")
 
 
-@pytest.mark.parametrize("rows,cols,batch", [(375, 1242, 0), (375, 1242, 129), (8, 1242, 1), (375, 4096, 1)])
+@pytest.mark.parametrize("rows,cols,batch", [(375, 1242, 0), (375, 1242, 513), (8, 1242, 1), (375, 4096, 1)])
 def test_create_rejects_bad_sizes_before_touching_the_gpu(vo, rows, cols, batch):
-    """vo_create validates image size (16..2048 per side) and max_batch (1..128) before any HIP
+    """vo_create validates image size (16..2048 per side) and max_batch (1..VO_MAX_BATCH) before any HIP
     call, returning NULL with the reason in vo_last_error(NULL) -- no GPU needed."""
     lib = vo.load_library()
     h = lib.vo_create(0, rows, cols, batch, None, None, None, None)
