@@ -4,8 +4,8 @@
 Workload (BASELINE.json configs[1]): SIFT detect+describe of both images +
 stereo matchFeatures, on 1242x375 synthetic stereo pairs (~2k keypoints per
 image), via libvo.so (hand-written HIP, gfx950).  One step = one batch of
-`--batch` independent stereo frames already resident in HBM (default 128, the
-library's largest batch: +1.4 % over 64 on one box, profiles/r05_o_batch.txt).  With --gpus N
+`--batch` independent stereo frames already resident in HBM (default 256: +1.4 % at 128 over
+64, +4.1-6.6 % at 256 over 128, 512 slower again -- profiles/r05_o_batch.txt).  With --gpus N
 (one process per GPU, RCCL; under torchrun, or bench.py starts torchrun itself
 when WORLD_SIZE is unset) each rank processes its own frames: weak scaling, no
 data-path collective; value = all frames / max-over-ranks time.
@@ -21,7 +21,7 @@ per-frame records all-gathered, poses chained on every rank, each rank's landmar
 rows moved to the world on its device and gathered to rank 0; it reports the reference's lagged xz error
 (PlotOnMap.m:8-20) and ATE against that trajectory (--seq-frames; 0 skips), and
 `large` the 1920x1080 / ~8k keypoint configuration (configs[4]) per GPU with the
-i8-MFMA rate of its dense stereo match block (--large-batch, default 64; 0 skips).
+i8-MFMA rate of its dense stereo match block (--large-batch, default 128; 0 skips).
 """
 from __future__ import annotations
 
@@ -59,10 +59,10 @@ TRAFFIC_FILE = max(ROOT.glob("profiles/r*_pmc_traffic.json"), key=_traffic_key,
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20, help="timed steps per run (--batch frames each: 2560 frames per run at 128)")
+    ap.add_argument("--steps", type=int, default=20, help="timed steps per run (--batch frames each: 5120 frames per run at 256)")
     ap.add_argument("--runs", type=int, default=5, help="timed runs of --steps steps; value = the median run (SURVEY §8d)")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=128, help="stereo frames per step (library maximum 128)")
+    ap.add_argument("--batch", type=int, default=256, help="stereo frames per step (library maximum VO_MAX_BATCH = 512)")
     ap.add_argument("--cpu-frames", type=int, default=32, help="frames in the CPU-oracle baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline (the box's share)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -73,7 +73,7 @@ def parse():
     ap.add_argument("--seq-batch", type=int, default=64, help="frames per vo_step_submit_dev call in the sequence leg")
     ap.add_argument("--dry-run", action="store_true",
                     help="rendezvous only (gloo, no GPU): rank 0 prints the world size it sees (launcher test)")
-    ap.add_argument("--large-batch", type=int, default=64,
+    ap.add_argument("--large-batch", type=int, default=128,
                     help="1920x1080 (~8k keypoints) stereo pairs per step for the configs[4] figure (0: skip)")
     return ap.parse_args()
 

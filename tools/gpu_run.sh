@@ -86,14 +86,14 @@ for st in $STEPS; do
     echo pmc-done ;;
   sbusy)
     # per-stream occupancy of the back-to-back loop (tools/stream_busy.py): which stream is critical
-    timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $O/strace -o t -- python3 tools/prof_run.py ${PMC_BATCH:-128} 6 > $O/strace.log 2>&1 \
+    timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $O/strace -o t -- python3 tools/prof_run.py ${PMC_BATCH:-256} 6 > $O/strace.log 2>&1 \
       || { tail -20 $O/strace.log; exit 1; }
     python3 tools/stream_busy.py $(find $O/strace -name "*kernel_trace.csv" | head -1) > $O/stream_busy.txt
     find $O/strace -name "*.csv" -delete
     cat $O/stream_busy.txt ;;
   insitu)
     # kernel trace of the asynchronous loop + the counter passes -> tools/insitu_model.py
-    timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $O/itrace -o t -- python3 tools/prof_run.py ${PMC_BATCH:-128} 6 > $O/itrace.log 2>&1 \
+    timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $O/itrace -o t -- python3 tools/prof_run.py ${PMC_BATCH:-256} 6 > $O/itrace.log 2>&1 \
       || { tail -20 $O/itrace.log; exit 1; }
     timeout -k 10 900 bash tools/pmc_passes.sh _$(basename $O) > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
     python3 tools/insitu_model.py gpurun_out/pmc_$(basename $O) $(find $O/itrace -name "*kernel_trace.csv" | head -1) $O/insitu.json
