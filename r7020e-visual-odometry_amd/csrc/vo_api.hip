@@ -85,6 +85,7 @@ struct vo_ctx {
         GeomBuffers gb;
     } aux;
     hipEvent_t ev_done[2] = {};
+    hipEvent_t ev_arena[2] = {};     // set's scale-space arena read for the last time (after k_desc)
     int next_set = 0, last_set = 0;
     Pyramid py;
     Pyramid* d_py = nullptr;
@@ -199,6 +200,8 @@ static void destroy_streams(vo_ctx* c)
     c->ev_fork = nullptr;
     for (int k = 0; k < 2; ++k) {
         if (c->ev_done[k]) hipEventDestroy(c->ev_done[k]);
+        if (c->ev_arena[k]) hipEventDestroy(c->ev_arena[k]);
+        c->ev_arena[k] = nullptr;
         if (c->ev_step[k]) hipEventDestroy(c->ev_step[k]);
         c->ev_done[k] = nullptr; c->ev_step[k] = nullptr;
     }
@@ -277,6 +280,7 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
     if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess) return bail("event", e);
     for (int k = 0; k < 2; ++k) {
         if ((e = hipEventCreateWithFlags(&c->ev_done[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
+        if ((e = hipEventCreateWithFlags(&c->ev_arena[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
         if ((e = hipEventCreateWithFlags(&c->ev_step[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
     }
     if ((e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking)) != hipSuccess) return bail("stream", e);
@@ -652,6 +656,9 @@ static SetRef set_ref(vo_ctx* c, int set)
 // slower: the feature stream is the critical one at 128 frames per step); 2 on a
 // stream of their own (sub[2]) after the level blurs, so neither stream waits for its
 // placement -- only the extremum test of the small octaves does.
+#ifndef VO_ARENA_EVENT
+#define VO_ARENA_EVENT 1          // the scale space of a set waits for its arena's last reader, not the whole feature stream
+#endif
 #ifndef VO_SMALL_STREAM
 #define VO_SMALL_STREAM 0
 #endif
@@ -666,7 +673,14 @@ static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uin
         HIPC(c, hipEventRecord(c->ev_fork, c->stream));
         HIPC(c, hipStreamWaitEvent(sp, c->ev_fork, 0));
     }
+#if VO_ARENA_EVENT
+    // the set's arena free: its previous call's last reader (k_desc) is done -- the stereo match
+    // of that call (descriptors only) may still run; everything else of the set is written by st,
+    // in order behind it
+    HIPC(c, hipStreamWaitEvent(sp, c->ev_arena[set], 0));
+#else
     HIPC(c, hipStreamWaitEvent(sp, c->ev_done[set], 0));      // set free (its previous features done)
+#endif
     const int o_small = sift_small_octave(c->py);
     const bool ext_on_st = VO_EXT_SPLIT || VO_SMALL_STREAM != 0;   // the test of octaves 1.. on st
     // scale space on sp; octave 0's extremum test on st as soon as octave 0 is built (beside the
@@ -703,6 +717,7 @@ static int enqueue_sift_stereo(vo_ctx* c, int set, const uint8_t* d_l, const uin
             sift_enqueue_extrema(c->py, v, 2 * nf, c->sp, st, c->d_py, o_small, c->py.n_oct);
         }
         sift_enqueue_features(c->py, v, 2 * nf, c->sp, st, c->d_py);
+        if (p == parts - 1) HIPC(c, hipEventRecord(c->ev_arena[set], st));
         match_launch(match_view(*S.mb, f0), S.jobs + f0, nf, c->mp, st);
     }
     HIPC(c, hipEventRecord(c->ev_done[set], st));
