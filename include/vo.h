@@ -70,6 +70,11 @@ extern "C" {
 #define VO_ERR_CAPACITY       -5
 #define VO_ERR_STATE          -6
 
+/* vo_step_out.flags / vo_pair_stats.flags: a capacity was exceeded and the frame's feature
+ * sets are incomplete (results then differ from an uncapped run) */
+#define VO_FLAG_KEYPOINTS   1    /* an image detected more than max_keypoints keypoints */
+#define VO_FLAG_CANDIDATES  2    /* an image's extremum candidates exceeded 4 x max_keypoints */
+
 #define VO_DESC_LEN 128
 #define VO_MAX_BATCH 512         /* largest max_batch of vo_create */
 
@@ -203,7 +208,7 @@ typedef struct {
     int32_t n_tracked;       /* K after find_remaining_points (0 on frame 1) */
     int32_t n_inliers;       /* MSAC inliers */
     int32_t n_landmarks;     /* landmark rows appended this frame */
-    int32_t pad;
+    int32_t flags;           /* VO_FLAG_* capacity flags of this frame's two images */
     double  rel_pose[16];    /* rel_pose.A (identity on frame 1) */
     double  pose[16];        /* world pose after this frame (pose.A) */
 } vo_step_out;
@@ -287,7 +292,7 @@ int vo_set_frame_index(vo_ctx* ctx, long frame_index);
 
 /* ---- benchmark workload: SIFT + stereo match on B independent pairs ---- */
 typedef struct {
-    int32_t n_left, n_right, n_stereo, flags;
+    int32_t n_left, n_right, n_stereo, flags;   /* flags: VO_FLAG_* */
 } vo_pair_stats;
 
 /* Device buffers: d_lefts/d_rights are B tightly packed rows*cols images.

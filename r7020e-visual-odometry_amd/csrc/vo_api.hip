@@ -2,6 +2,7 @@
 // orchestration of the per-frame pipeline on one HIP stream.
 #include "vo_internal.h"
 #include "vo_geom.h"
+#include <climits>
 #include <cstdio>
 #include <cstring>
 #include <cstdarg>
@@ -116,7 +117,7 @@ struct vo_ctx {
     // Per set: pinned host copies of the per-frame results and the event that ends the
     // batch (geometry, carry into the other set, result copies).
     struct StepHost {
-        FrameGeom* fg = nullptr; int* nkp = nullptr; int* np = nullptr; int* rows = nullptr;
+        FrameGeom* fg = nullptr; int* nkp = nullptr; int* ncand = nullptr; int* np = nullptr; int* rows = nullptr;
         float* pX = nullptr; uint8_t* pkeep = nullptr;   // the batch's packed landmark rows (pinned)
     };
     StepHost sh[2];
@@ -218,7 +219,7 @@ static void destroy_buffers(vo_ctx* c)
     hipFree(c->aux.d_jobs); hipFree(c->aux.pair_i); hipFree(c->aux.pair_j); hipFree(c->aux.pair_n);
     geom_free(c->aux.gb);
     for (int k = 0; k < 2; ++k) {
-        hipHostFree(c->sh[k].fg); hipHostFree(c->sh[k].nkp); hipHostFree(c->sh[k].np); hipHostFree(c->sh[k].rows);
+        hipHostFree(c->sh[k].fg); hipHostFree(c->sh[k].nkp); hipHostFree(c->sh[k].ncand); hipHostFree(c->sh[k].np); hipHostFree(c->sh[k].rows);
         hipHostFree(c->sh[k].pX); hipHostFree(c->sh[k].pkeep);
         c->sh[k] = vo_ctx::StepHost();
     }
@@ -361,6 +362,7 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
         vo_ctx::StepHost& H = c->sh[k];
         if ((e = hipHostMalloc((void**)&H.fg, sizeof(FrameGeom) * max_batch, 0)) != hipSuccess) return bail("pinned", e);
         if ((e = hipHostMalloc((void**)&H.nkp, sizeof(int) * 2 * max_batch, 0)) != hipSuccess) return bail("pinned", e);
+        if ((e = hipHostMalloc((void**)&H.ncand, sizeof(int) * 2 * max_batch, 0)) != hipSuccess) return bail("pinned", e);
         if ((e = hipHostMalloc((void**)&H.np, sizeof(int) * max_batch, 0)) != hipSuccess) return bail("pinned", e);
         if ((e = hipHostMalloc((void**)&H.rows, sizeof(int) * max_batch, 0)) != hipSuccess) return bail("pinned", e);
         if ((e = hipHostMalloc((void**)&H.pX, sizeof(float) * 3 * max_batch * kp_cap, 0)) != hipSuccess) return bail("pinned", e);
@@ -510,8 +512,9 @@ int vo_sift_ex(vo_ctx* c, const uint8_t* img, int rows, int cols, int ld, int co
     ImageSrc src{c->d_img, c->d_img, (size_t)rows * cols, cols, 0};
     sift_enqueue(c->py, c->sb, src, 1, c->sp, c->stream, c->d_py);
     c->last_set = 0;                                   // vo_fetch_* now read this result (set 0)
-    int n = 0;
+    int n = 0, n_cand = 0;
     HIPC(c, hipMemcpyAsync(&n, c->sb.n_kp, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(&n_cand, c->sb.n_cand, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     int rc = finish(c);
     if (rc) return rc;
     if (n_out) *n_out = n;
@@ -520,6 +523,9 @@ int vo_sift_ex(vo_ctx* c, const uint8_t* img, int rows, int cols, int ld, int co
         if (kps) HIPC(c, hipMemcpy(kps, c->sb.kp, sizeof(vo_keypoint) * m, hipMemcpyDeviceToHost));
         if (desc) HIPC(c, hipMemcpy(desc, c->sb.desc, (size_t)m * VO_DESC_LEN, hipMemcpyDeviceToHost));
     }
+    if (n_cand > c->sb.cand_cap)
+        return fail(c, VO_ERR_CAPACITY, "vo_sift: %d extremum candidates exceed the candidate list (%d = 4 x max_keypoints)",
+                    n_cand, c->sb.cand_cap);
     if (n > c->sb.kp_cap) return fail(c, VO_ERR_CAPACITY, "vo_sift: %d keypoints exceed max_keypoints %d", n, c->sb.kp_cap);
     if (n > capacity) return fail(c, VO_ERR_CAPACITY, "vo_sift: %d keypoints exceed capacity %d", n, capacity);
     return VO_OK;
@@ -624,6 +630,20 @@ int vo_match_f32(vo_ctx* c, const float* F1, int n1, int ld1, const float* F2, i
 
 // SIFT + stereo match on B frames already in device memory.
 // buffers of set `set` of the asynchronous batch pipeline
+// vo_pair_stats.flags / vo_step_out.flags of one frame's n images: VO_FLAG_KEYPOINTS if an
+// image detected more keypoints than max_keypoints, VO_FLAG_CANDIDATES if its extremum test
+// (k_ext_inner's partial candidates included) produced more candidates than the list holds,
+// so k_seg_emit dropped some in scan order and the keypoint set is incomplete
+static int capacity_flags(const SiftBuffers& sb, const int* nkp, const int* ncand, int n)
+{
+    int fl = 0;
+    for (int i = 0; i < n; ++i) {
+        if (nkp[i] > sb.kp_cap) fl |= VO_FLAG_KEYPOINTS;
+        if (ncand[i] > sb.cand_cap) fl |= VO_FLAG_CANDIDATES;
+    }
+    return fl;
+}
+
 struct SetRef {
     SiftBuffers* sb; MatchBuffers* mb; MatchJob* jobs; int* pair_i; int* pair_j; int* pair_n;
     GeomBuffers* gb; MatchJob* track_jobs;
@@ -743,15 +763,16 @@ int vo_sift_match_batch_dev(vo_ctx* c, const uint8_t* d_lefts, const uint8_t* d_
         return VO_OK;
     }
     SetRef S = set_ref(c, set);
-    std::vector<int> nk(2 * B), np(B);
+    std::vector<int> nk(2 * B), nc(2 * B), np(B);
     HIPC(c, hipMemcpyAsync(nk.data(), S.sb->n_kp, sizeof(int) * 2 * B, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(nc.data(), S.sb->n_cand, sizeof(int) * 2 * B, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(np.data(), S.pair_n, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
     rc = finish(c);
     if (rc) return rc;
     if (stats) {
         for (int f = 0; f < B; ++f) {
             stats[f].n_left = nk[2 * f]; stats[f].n_right = nk[2 * f + 1]; stats[f].n_stereo = np[f];
-            stats[f].flags = (nk[2 * f] > c->sb.kp_cap || nk[2 * f + 1] > c->sb.kp_cap) ? 1 : 0;
+            stats[f].flags = capacity_flags(c->sb, nk.data() + 2 * f, nc.data() + 2 * f, 2);
         }
     }
     return VO_OK;
@@ -908,6 +929,7 @@ static int submit_batch(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B
     vo_ctx::StepHost& H = c->sh[set];
     HIPC(c, hipMemcpyAsync(H.fg, S.gb->fg, sizeof(FrameGeom) * B, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(H.nkp, S.sb->n_kp, sizeof(int) * 2 * B, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(H.ncand, S.sb->n_cand, sizeof(int) * 2 * B, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(H.np, S.pair_n, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(H.rows, S.gb->lm_rows, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
     lm_pack_launch(*S.gb, B, c->stream);
@@ -958,11 +980,17 @@ static int collect_batch(vo_ctx* c, vo_step_out* outs, int capacity, int* n_out)
                     hipFree(nX);
                     return fail(c, VO_ERR_HIP, "vo_step_collect: landmark store of %zu rows", cap);
                 }
+                // the store at least doubles, so this synchronising growth happens O(log rows) times
+                hipError_t ge = hipSuccess;
                 if (c->lm_n > 0) {
-                    HIPC(c, hipMemcpyAsync(nX, c->d_lmX, sizeof(float) * 3 * c->lm_n, hipMemcpyDeviceToDevice, c->stream));
-                    HIPC(c, hipMemcpyAsync(nk, c->d_lmkeep, c->lm_n, hipMemcpyDeviceToDevice, c->stream));
+                    ge = hipMemcpyAsync(nX, c->d_lmX, sizeof(float) * 3 * c->lm_n, hipMemcpyDeviceToDevice, c->stream);
+                    if (ge == hipSuccess) ge = hipMemcpyAsync(nk, c->d_lmkeep, c->lm_n, hipMemcpyDeviceToDevice, c->stream);
                 }
-                HIPC(c, hipStreamSynchronize(c->stream));
+                if (ge == hipSuccess) ge = hipStreamSynchronize(c->stream);
+                if (ge != hipSuccess) {
+                    hipFree(nX); hipFree(nk);
+                    return fail(c, VO_ERR_HIP, "vo_step_collect: landmark store growth: %s", hipGetErrorString(ge));
+                }
                 hipFree(c->d_lmX); hipFree(c->d_lmkeep);
                 c->d_lmX = nX; c->d_lmkeep = nk; c->lm_cap = cap;
             }
@@ -983,6 +1011,7 @@ static int collect_batch(vo_ctx* c, vo_step_out* outs, int capacity, int* n_out)
         vo_step_out& o = outs[f];
         memset(&o, 0, sizeof(o));
         o.n_left = H.nkp[2 * f]; o.n_right = H.nkp[2 * f + 1]; o.n_stereo = H.np[f];
+        o.flags = capacity_flags(c->sb, H.nkp + 2 * f, H.ncand + 2 * f, 2);
         memcpy(o.rel_pose, I4, sizeof(I4));
         const bool tracked = f > 0 || P.first_tracked;
         if (c->lm_camera) {
@@ -1143,6 +1172,8 @@ int vo_get_landmark_rows(vo_ctx* c, float* X, uint8_t* keep, int capacity, int* 
     if (!c || capacity < 0) return fail(c, VO_ERR_ARG, "vo_get_landmark_rows: bad arguments");
     if (!c->lm_camera) return fail(c, VO_ERR_STATE, "vo_get_landmark_rows: context keeps world rows (vo_set_landmark_frame(ctx, 1) first)");
     if (!c->pending.empty()) return fail(c, VO_ERR_STATE, "vo_get_landmark_rows: batches pending");
+    if (c->lm_n > (size_t)INT_MAX)    // the device store is size_t; this API counts in int (vo_landmarks_world_dev: long)
+        return fail(c, VO_ERR_CAPACITY, "vo_get_landmark_rows: %zu rows exceed INT_MAX (use vo_landmarks_world_dev)", c->lm_n);
     const int r = (int)c->lm_n;
     if (rows) *rows = r;
     const int m = std::min(r, capacity);

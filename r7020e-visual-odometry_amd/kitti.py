@@ -344,6 +344,8 @@ def run_shard(seq, rank: int, world: int, batch: int = 16, device: int | None = 
     for `finish_shard` and X, keep are None."""
     import torch
     from . import sharding, vo
+    if not rows_to_host and ctx is None:        # checked before any context or frame work
+        raise ValueError("run_shard: rows_to_host=False needs a caller-owned ctx (the rows live in it)")
     device = _local_device() if device is None else device
     on_device = isinstance(seq, tuple)
     n_all = seq[0].shape[0] if on_device else len(seq)
@@ -359,8 +361,6 @@ def run_shard(seq, rank: int, world: int, batch: int = 16, device: int | None = 
     ctx.set_frame_index(h)
     src = device_batches(seq[0], seq[1], batch, h, e) if on_device else seq.batches(batch, h, e)
     outs = _pipelined(ctx, src, torch.device("cuda", device))
-    if not rows_to_host and own:
-        raise ValueError("run_shard: rows_to_host=False needs a caller-owned ctx (the rows live in it)")
     X, keep = ctx.get_landmark_rows() if rows_to_host else (None, None)
     if own:
         ctx.close()
@@ -427,7 +427,12 @@ def finish_shard(ctx, outs, n: int, rank: int, world: int, device: int, group=No
     m = max(max(counts), 1)
     buf = torch.empty((m, 3), dtype=torch.float32, device=torch.device("cuda", device))
     rows = ctx.landmarks_world_dev(poses[h:e], buf.data_ptr(), m)
-    if rows != counts[rank]:
+    bad = rows != counts[rank]
+    if distributed and sharding.any_rank(bad, group=group, device=collective_device):
+        # every rank learns of a mismatch before the gather, so none is left waiting in it
+        raise RuntimeError(f"rank {rank}: {rows} landmark rows on the device, records say {counts[rank]}"
+                           + ("" if bad else " on another rank"))
+    if bad:
         raise RuntimeError(f"rank {rank}: {rows} landmark rows on the device, records say {counts[rank]}")
     t3 = time.perf_counter()
     if not distributed:

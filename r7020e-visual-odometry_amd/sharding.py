@@ -124,6 +124,18 @@ def rank_row_counts(n_landmarks, n_frames: int, world: int) -> list[int]:
     return [int(n_landmarks[slice(*shard_range(n_frames, world, r))].sum()) for r in range(world)]
 
 
+def any_rank(flag: bool, group=None, device=None) -> bool:
+    """True on every rank of the group if `flag` is true on any (one MAX all-reduce of a
+    single int: on `device` for RCCL, on the CPU for gloo).  Ranks agree on an error before a
+    collective that a failing rank would otherwise leave the others waiting in."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32,
+                     device=torch.device("cpu") if device is None else torch.device(device))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return bool(t.item())
+
+
 def gather_rows_to_root(rows_local, counts, group=None, device=None, out=None):
     """Rank 0 of the group receives every rank's world landmark rows (float32 [counts[r], 3], rank
     order = frame order) as one host array; the other ranks get None.  One dist.gather of

@@ -69,7 +69,7 @@ class Keypoint(C.Structure):
 class StepOut(C.Structure):
     _fields_ = [("status", C.c_int32), ("n_left", C.c_int32), ("n_right", C.c_int32),
                 ("n_stereo", C.c_int32), ("n_tracked", C.c_int32), ("n_inliers", C.c_int32),
-                ("n_landmarks", C.c_int32), ("pad", C.c_int32),
+                ("n_landmarks", C.c_int32), ("flags", C.c_int32),
                 ("rel_pose", C.c_double * 16), ("pose", C.c_double * 16)]
 
 
@@ -80,7 +80,7 @@ class PairStats(C.Structure):
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
                      ("octave", "<i4"), ("layer", "<i4"), ("scale", "<f4")])
 STEP_DTYPE = np.dtype([("status", "<i4"), ("n_left", "<i4"), ("n_right", "<i4"), ("n_stereo", "<i4"),
-                       ("n_tracked", "<i4"), ("n_inliers", "<i4"), ("n_landmarks", "<i4"), ("pad", "<i4"),
+                       ("n_tracked", "<i4"), ("n_inliers", "<i4"), ("n_landmarks", "<i4"), ("flags", "<i4"),
                        ("rel_pose", "<f8", (4, 4)), ("pose", "<f8", (4, 4))])
 
 # exported symbols (tests check the library exports every one)

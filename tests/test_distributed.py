@@ -111,3 +111,35 @@ def test_sharded_street_sequence_poses_and_landmarks_equal_single_process(street
     path, outs, lm = street_seq
     assert (outs["status"][1:] == 0).all() and len(lm) > 100
     _check(_run(world, path), outs, lm)
+
+
+def _agree_worker(rank, world, port, result_q):
+    sys.path.insert(0, str(ROOT))
+    import torch.distributed as dist
+    import vo_amd  # noqa: F401
+    from r7020e_visual_odometry_amd import sharding
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # only the last rank fails its check; every rank must learn of it before a later collective
+    res = (sharding.any_rank(False), sharding.any_rank(rank == world - 1))
+    result_q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ranks_agree_on_an_error_before_the_gather():
+    """kitti.finish_shard raises on every rank when one rank's landmark row count disagrees
+    with the records (sharding.any_rank), instead of leaving the others inside dist.gather."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(got[r] == (False, True) for r in range(world)), got

@@ -198,3 +198,27 @@ def test_create_refuses_sigma_beyond_the_orientation_bound(vo):
     p = vo.default_sift_params()
     p.sigma = 4.0                                      # well inside the bound: accepted
     vo.Context(64, 64, 1, sift=p).close()
+
+
+def test_candidate_overflow_is_reported(vo, syn):
+    """With max_keypoints small enough that the candidate list (4 x max_keypoints) overflows,
+    the extremum candidates k_seg_emit drops are reported: VO_FLAG_CANDIDATES in the batch
+    stats and VO_ERR_CAPACITY from vo_sift (a truncated keypoint set never passes silently);
+    the default capacity reports nothing."""
+    import torch
+    L, R = syn.independent_pairs(2, px_per_cell=syn.BENCH_PX_PER_CELL)
+    dl = torch.from_numpy(L).cuda()
+    dr = torch.from_numpy(R).cuda()
+    torch.cuda.synchronize()
+    small = vo.Context(375, 1242, 2, sift=vo.default_sift_params(64))
+    st = small.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), 2)
+    assert all(s[3] & 2 for s in st), st            # VO_FLAG_CANDIDATES
+    assert all(s[3] & 1 for s in st), st            # and the keypoints themselves overflow
+    with pytest.raises(vo.VOError) as e:
+        small.sift(L[0])
+    assert e.value.code == vo.VO_ERR_CAPACITY and "candidates" in str(e.value)
+    small.close()
+    full = vo.Context(375, 1242, 2)
+    st = full.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), 2)
+    assert all(s[3] == 0 for s in st), st
+    full.close()

@@ -108,7 +108,7 @@ def test_misaligned_image_pointers(vo, oracle, syn, offset):
 
 
 def test_batch_128_equals_two_batches_of_64(vo, oracle, syn):
-    """The largest batch (128 frames = 256 images + 2 carry slots in one scale-space arena)
+    """A 128-frame batch (256 images + 2 carry slots in one scale-space arena)
     gives the same keypoints, descriptors and stereo matches as the same frames in two
     64-frame calls; frames at both ends are also checked against the oracle."""
     import torch
@@ -143,3 +143,56 @@ def test_batch_128_equals_two_batches_of_64(vo, oracle, syn):
     for f in (0, B - 1):
         rkl, rdl = oracle.sift(L[f])
         assert np.array_equal(got[f][0], rkl) and np.array_equal(got[f][1], rdl), f
+
+
+def test_bench_batches_256_and_512_equal_64_frame_calls(vo, oracle, syn):
+    """The bench's own configuration: one 256-frame call (bench.py's default --batch) and one
+    512-frame call (VO_MAX_BATCH; 1024 images + 2 carry slots, so `flat_find_wave`'s image
+    search runs far past 258 slots) give every frame's keypoints, descriptors and stereo pairs
+    exactly as the same frames in eight 64-frame calls; the first, a middle and the last frame
+    are also checked against the oracle (VO.m:79-87).  128 rendered pairs are reused four times,
+    each reuse rolled by a different column shift, so every one of the 512 frames is distinct."""
+    import torch
+    B = 512
+    U = 128
+    L0, R0 = syn.independent_pairs(U, px_per_cell=syn.BENCH_PX_PER_CELL, threads=16)
+    L = np.concatenate([np.roll(L0, 37 * k, axis=2) for k in range(B // U)])
+    R = np.concatenate([np.roll(R0, 37 * k, axis=2) for k in range(B // U)])
+    dl = torch.from_numpy(L).cuda()
+    dr = torch.from_numpy(R).cuda()
+    torch.cuda.synchronize()
+    fs = L[0].size
+
+    def collect(ctx, n):
+        out = []
+        for f in range(n):
+            kl, dsl = ctx.fetch_keypoints(2 * f)
+            kr, dsr = ctx.fetch_keypoints(2 * f + 1)
+            out.append((kl, dsl, kr, dsr, ctx.fetch_stereo_pairs(f)))
+        return out
+
+    small = vo.Context(375, 1242, 64)
+    ref = []
+    for b0 in range(0, B, 64):
+        small.sift_match_batch_dev(dl.data_ptr() + b0 * fs, dr.data_ptr() + b0 * fs, 64)
+        ref += collect(small, 64)
+    small.close()
+    assert min(len(r[0]) for r in ref) > 1000
+
+    for n in (256, 512):
+        ctx = vo.Context(375, 1242, n)
+        stats = ctx.sift_match_batch_dev(dl.data_ptr(), dr.data_ptr(), n)
+        got = collect(ctx, n)
+        ctx.close()
+        for f in range(n):
+            assert stats[f][2] == len(ref[f][4]), (n, f)
+            for a, b in zip(got[f], ref[f]):
+                assert np.array_equal(a, b), (n, f)
+
+    for f in (0, 255, B - 1):
+        rkl, rdl = oracle.sift(L[f])
+        rkr, rdr = oracle.sift(R[f])
+        _same_kps(ref[f][0], rkl)
+        _same_kps(ref[f][2], rkr)
+        assert np.array_equal(ref[f][1], rdl) and np.array_equal(ref[f][3], rdr), f
+        assert np.array_equal(ref[f][4], oracle.match(rdl, rdr)), f
