@@ -77,6 +77,7 @@ extern "C" {
 
 #define VO_DESC_LEN 128
 #define VO_MAX_BATCH 512         /* largest max_batch of vo_create */
+#define VO_STEP_DEPTH 3          /* batches vo_step_submit_dev keeps in flight */
 
 /* detectSIFTFeatures / extractFeatures defaults (MATLAB R2022b+).
  * contrast_threshold is in OpenCV units: MATLAB's ContrastThreshold 0.0133
@@ -234,8 +235,9 @@ int vo_step_batch_dev(vo_ctx* ctx, const uint8_t* d_lefts, const uint8_t* d_righ
  * device half of B frames and returns; collect waits for the oldest submitted batch and
  * runs the host half (pose chain, landmark append), writing its B outputs.  Consecutive
  * batches alternate two buffer sets, so batch n+1's SIFT overlaps batch n's tracking /
- * MSAC / landmark kernels and the host work of collect(n).  At most two batches may be
- * pending (submit(n+2) needs collect(n) first); other calls on the context are refused
+ * MSAC / landmark kernels and the host work of collect(n); batch n+2's SIFT waits for batch
+ * n's geometry on the device, not for collect(n).  At most VO_STEP_DEPTH (3) batches may be
+ * pending (submit(n+3) needs collect(n) first); other calls on the context are refused
  * while any is pending.  Inputs of a submit made while another batch is pending must be
  * ready on the device at the call (the first submit is ordered after vo_stream()). */
 int vo_step_submit_dev(vo_ctx* ctx, const uint8_t* d_lefts, const uint8_t* d_rights, int B);
@@ -243,7 +245,8 @@ int vo_step_collect(vo_ctx* ctx, vo_step_out* outs, int capacity, int* n);
 int vo_steps_pending(const vo_ctx* ctx);
 
 /* Visualisation data of frame `frame` of the most recently collected batch (valid until
- * that buffer set is reused, i.e. the next-but-one submit): the tracked points'
+ * that buffer set is reused, i.e. the next-but-one submit; VO_ERR_STATE once that batch is
+ * submitted, so a driver that visualises keeps at most two batches pending): the tracked points'
  * previous-frame left positions, current left image points and triangulated world points
  * (remaining_old_features.l_pos / .pos of VO.m:106-116), and every current left detection
  * (l_pos, VO.m:79).  Any output pointer may be NULL. */

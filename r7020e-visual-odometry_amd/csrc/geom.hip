@@ -49,8 +49,6 @@ hipError_t geom_alloc(GeomBuffers& g, int max_frames, int kp_cap, int n_hyp)
     GA(g.lm_X, sizeof(float) * F * K * 3);
     GA(g.lm_keep, F * K);
     GA(g.lm_rows, sizeof(int) * F);
-    GA(g.lm_pX, sizeof(float) * F * K * 3);
-    GA(g.lm_pkeep, F * K);
 #undef GA
     e = hipMemset(g.step_n, 0, sizeof(int) * 4 * F);
     if (e != hipSuccess) return e;
@@ -60,7 +58,7 @@ hipError_t geom_alloc(GeomBuffers& g, int max_frames, int kp_cap, int n_hyp)
 void geom_free(GeomBuffers& g)
 {
     void* bufs[] = {g.lists, g.list_n, g.step_i, g.step_j, g.step_n, g.world, g.imgpt, g.oldpos, g.inliers, g.hyp,
-                    g.fg, g.spos, g.s_n, g.lm_new, g.lm_M, g.lm_X, g.lm_keep, g.lm_rows, g.lm_pX, g.lm_pkeep};
+                    g.fg, g.spos, g.s_n, g.lm_new, g.lm_M, g.lm_X, g.lm_keep, g.lm_rows};
     for (void* p : bufs) (void)hipFree(p);   // teardown: nothing to report to
     g = GeomBuffers();
 }
@@ -991,9 +989,9 @@ __global__ __launch_bounds__(256) void k_lm_pack(const float* __restrict__ lm_X,
     for (int e = tid; e < n; e += 256) pkeep[off + e] = lm_keep[(size_t)f * kp_cap + e];
 }
 
-void lm_pack_launch(GeomBuffers& g, int B, hipStream_t s)
+void lm_pack_launch(GeomBuffers& g, int B, float* pX, uint8_t* pkeep, hipStream_t s)
 {
-    VO_LAUNCH(k_lm_pack, dim3(B), dim3(256), 0, s, g.lm_X, g.lm_keep, g.lm_rows, g.kp_cap, g.lm_pX, g.lm_pkeep);
+    VO_LAUNCH(k_lm_pack, dim3(B), dim3(256), 0, s, g.lm_X, g.lm_keep, g.lm_rows, g.kp_cap, pX, pkeep);
 }
 
 // block f: frame f's rows, one thread per row.  The f64 products and sums are those of the host

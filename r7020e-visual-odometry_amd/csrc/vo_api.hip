@@ -113,19 +113,23 @@ struct vo_ctx {
     int* d_mi = nullptr; int* d_mj = nullptr; int* d_mn = nullptr;
     GeomBuffers gb;
     // Pipelined full path (vo_step_submit_dev / vo_step_collect): batch n uses buffer set
-    // n & 1; its geometry runs on `stream` while the next batch's SIFT runs on sub[0..1].
-    // Per set: pinned host copies of the per-frame results and the event that ends the
-    // batch (geometry, carry into the other set, result copies).
+    // n & 1; its geometry runs on `stream` while the later batches' SIFT runs on sub[0..1].
+    // Up to VO_STEP_DEPTH batches are in flight, so each batch also owns a result slot
+    // (n mod VO_STEP_DEPTH): pinned host copies of the per-frame results, its packed landmark
+    // rows on the device, and the event that ends the batch (geometry, carry into the other
+    // set, result copies).  A slot outlives its buffer set's reuse by batch n+2.
     struct StepHost {
         FrameGeom* fg = nullptr; int* nkp = nullptr; int* ncand = nullptr; int* np = nullptr; int* rows = nullptr;
-        float* pX = nullptr; uint8_t* pkeep = nullptr;   // the batch's packed landmark rows (pinned)
+        float* pX = nullptr; uint8_t* pkeep = nullptr;     // the batch's packed landmark rows (pinned)
+        float* d_pX = nullptr; uint8_t* d_pkeep = nullptr; // ... and on the device (k_lm_pack)
+        hipEvent_t ev = nullptr;                           // end of the batch on `stream`
     };
-    StepHost sh[2];
-    hipEvent_t ev_step[2] = {};
+    StepHost sh[VO_STEP_DEPTH];
     hipStream_t copy_stream = nullptr;
-    struct Pending { int set, B; bool first_tracked; };
+    struct Pending { int set, slot, B; bool first_tracked; };
     std::deque<Pending> pending;
-    int next_step_set = 0;
+    int next_step_set = 0, next_slot = 0;
+    std::vector<void*> lm_retired;                   // landmark stores replaced by a larger one (freed at reset)
     int last_step_set = -1, last_step_B = 0;          // the most recently collected batch (vo_fetch_tracks)
     std::string err;
     Profiler prof;
@@ -203,8 +207,11 @@ static void destroy_streams(vo_ctx* c)
         if (c->ev_done[k]) hipEventDestroy(c->ev_done[k]);
         if (c->ev_arena[k]) hipEventDestroy(c->ev_arena[k]);
         c->ev_arena[k] = nullptr;
-        if (c->ev_step[k]) hipEventDestroy(c->ev_step[k]);
-        c->ev_done[k] = nullptr; c->ev_step[k] = nullptr;
+        c->ev_done[k] = nullptr;
+    }
+    for (int k = 0; k < VO_STEP_DEPTH; ++k) {
+        if (c->sh[k].ev) hipEventDestroy(c->sh[k].ev);
+        c->sh[k].ev = nullptr;
     }
     if (c->copy_stream) hipStreamDestroy(c->copy_stream);
     c->copy_stream = nullptr;
@@ -218,11 +225,16 @@ static void destroy_buffers(vo_ctx* c)
     match_free(c->aux.mb);
     hipFree(c->aux.d_jobs); hipFree(c->aux.pair_i); hipFree(c->aux.pair_j); hipFree(c->aux.pair_n);
     geom_free(c->aux.gb);
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < VO_STEP_DEPTH; ++k) {
         hipHostFree(c->sh[k].fg); hipHostFree(c->sh[k].nkp); hipHostFree(c->sh[k].ncand); hipHostFree(c->sh[k].np); hipHostFree(c->sh[k].rows);
         hipHostFree(c->sh[k].pX); hipHostFree(c->sh[k].pkeep);
+        hipFree(c->sh[k].d_pX); hipFree(c->sh[k].d_pkeep);
+        const hipEvent_t ev = c->sh[k].ev;               // owned by destroy_streams
         c->sh[k] = vo_ctx::StepHost();
+        c->sh[k].ev = ev;
     }
+    for (void* p : c->lm_retired) hipFree(p);
+    c->lm_retired.clear();
     geom_free(c->gb);
     hipFree(c->d_py); hipFree(c->d_jobs); hipFree(c->d_pair_i); hipFree(c->d_pair_j); hipFree(c->d_pair_n);
     hipFree(c->d_img); hipFree(c->d_cm); hipFree(c->d_fd[0]); hipFree(c->d_fd[1]); hipFree(c->d_fm[0]); hipFree(c->d_fm[1]);
@@ -282,7 +294,6 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
     for (int k = 0; k < 2; ++k) {
         if ((e = hipEventCreateWithFlags(&c->ev_done[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
         if ((e = hipEventCreateWithFlags(&c->ev_arena[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
-        if ((e = hipEventCreateWithFlags(&c->ev_step[k], hipEventDisableTiming)) != hipSuccess) return bail("event", e);
     }
     if ((e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking)) != hipSuccess) return bail("stream", e);
     const int n_slots = 2 * max_batch + 2;
@@ -358,8 +369,11 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
         if ((e = hipMemcpy(X.d_jobs, xj.data(), sizeof(MatchJob) * xn, hipMemcpyHostToDevice)) != hipSuccess)
             return bail("jobs copy (set 1)", e);
     }
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < VO_STEP_DEPTH; ++k) {
         vo_ctx::StepHost& H = c->sh[k];
+        if ((e = hipEventCreateWithFlags(&H.ev, hipEventDisableTiming)) != hipSuccess) return bail("event", e);
+        if ((e = hipMalloc((void**)&H.d_pX, sizeof(float) * 3 * max_batch * kp_cap)) != hipSuccess) return bail("packed rows", e);
+        if ((e = hipMalloc((void**)&H.d_pkeep, (size_t)max_batch * kp_cap)) != hipSuccess) return bail("packed rows", e);
         if ((e = hipHostMalloc((void**)&H.fg, sizeof(FrameGeom) * max_batch, 0)) != hipSuccess) return bail("pinned", e);
         if ((e = hipHostMalloc((void**)&H.nkp, sizeof(int) * 2 * max_batch, 0)) != hipSuccess) return bail("pinned", e);
         if ((e = hipHostMalloc((void**)&H.ncand, sizeof(int) * 2 * max_batch, 0)) != hipSuccess) return bail("pinned", e);
@@ -910,35 +924,43 @@ static int enqueue_carry(vo_ctx* c, int from, int f, int to)
 // The VO.m loop body for B frames whose images are in device memory, split into a
 // device half (submit: everything up to the per-frame results, asynchronous) and a host
 // half (collect: pose chain VO.m:130-134 and landmark append CreateLandmarksFromFeatures.m:20).
-// Batch n uses buffer set n & 1.  Its SIFT + stereo matching run on sub[0..1] and wait only
-// for the previous batch of the same set (collected before this submit); its tracking,
-// triangulation, MSAC and landmark kernels run on `stream` after the SIFT and after the
-// previous batch's carry; then frame B-1 is carried into the other set and the small
-// per-frame results are copied to pinned host memory.  With fork, the SIFT is also ordered
-// after earlier work on `stream` (the synchronous calls' H2D copies).
+// Batch n uses buffer set n & 1 and result slot n mod VO_STEP_DEPTH.  Its scale space (sub[0])
+// waits only for the arena's last reader of batch n-2 (ev_arena); its feature stages and stereo
+// matching (sub[1]) overwrite the keypoints, descriptors and stereo pairs that batch n-2's
+// geometry reads, so they wait for the end of that batch on the GPU (its slot event) -- not for
+// the host to collect it, so the scale space of batch n runs straight after batch n-1's while
+// batch n-2's geometry finishes.  Its tracking, triangulation, MSAC and landmark kernels run on
+// `stream` after the SIFT and after the previous batch's carry; then frame B-1 is carried into
+// the other set, the landmark rows are packed into the slot and the small per-frame results
+// are copied to the slot's pinned host memory.  With fork, the SIFT is also ordered after
+// earlier work on `stream` (the synchronous calls' H2D copies).
 static int submit_batch(vo_ctx* c, const uint8_t* d_l, const uint8_t* d_r, int B, bool fork)
 {
     if (!c->has_calib) return fail(c, VO_ERR_STATE, "vo_step: no calibration (vo_set_calib)");
-    if (c->pending.size() >= 2) return fail(c, VO_ERR_STATE, "vo_step_submit_dev: two batches already pending (collect first)");
-    const int set = c->next_step_set;
+    if (c->pending.size() >= VO_STEP_DEPTH)
+        return fail(c, VO_ERR_STATE, "vo_step_submit_dev: %d batches already pending (collect first)", VO_STEP_DEPTH);
+    const int set = c->next_step_set, slot = c->next_slot;
     SetRef S = set_ref(c, set);
+    for (const vo_ctx::Pending& q : c->pending)         // batch n-2 (same set), still in flight
+        if (q.set == set) HIPC(c, hipStreamWaitEvent(c->sub[1], c->sh[q.slot].ev, 0));
     int rc = enqueue_sift_stereo(c, set, d_l, d_r, B, true, fork);   // `stream` waits for this set's SIFT
     if (rc) return rc;
     StepArgs a = step_args(c, B, set);
     geom_enqueue(*S.gb, *S.mb, S.track_jobs, a, c->mp, c->stream);
-    vo_ctx::StepHost& H = c->sh[set];
+    vo_ctx::StepHost& H = c->sh[slot];
     HIPC(c, hipMemcpyAsync(H.fg, S.gb->fg, sizeof(FrameGeom) * B, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(H.nkp, S.sb->n_kp, sizeof(int) * 2 * B, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(H.ncand, S.sb->n_cand, sizeof(int) * 2 * B, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(H.np, S.pair_n, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(H.rows, S.gb->lm_rows, sizeof(int) * B, hipMemcpyDeviceToHost, c->stream));
-    lm_pack_launch(*S.gb, B, c->stream);
+    lm_pack_launch(*S.gb, B, H.d_pX, H.d_pkeep, c->stream);
     if ((rc = enqueue_carry(c, set, B - 1, set ^ 1))) return rc;
-    HIPC(c, hipEventRecord(c->ev_step[set], c->stream));
+    HIPC(c, hipEventRecord(H.ev, c->stream));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(c, VO_ERR_HIP, "launch: %s", hipGetErrorString(e));
-    c->pending.push_back({set, B, c->have_features});
+    c->pending.push_back({set, slot, B, c->have_features});
     c->next_step_set ^= 1;
+    c->next_slot = (slot + 1) % VO_STEP_DEPTH;
     c->have_features = true;
     c->frame_index += B;
     return VO_OK;
@@ -950,14 +972,13 @@ static int collect_batch(vo_ctx* c, vo_step_out* outs, int capacity, int* n_out)
     const vo_ctx::Pending P = c->pending.front();
     if (capacity < P.B) return fail(c, VO_ERR_CAPACITY, "vo_step_collect: %d frames pending, capacity %d", P.B, capacity);
     const int K = c->sb.kp_cap, B = P.B;
-    SetRef S = set_ref(c, P.set);
-    const vo_ctx::StepHost& H = c->sh[P.set];
+    const vo_ctx::StepHost& H = c->sh[P.slot];
     if (c->prof.on) {                                  // profiling: events of every stream are collected
         g_prof = &c->prof;
         int rc = finish(c);
         if (rc) return rc;
     } else {
-        HIPC(c, hipEventSynchronize(c->ev_step[P.set]));
+        HIPC(c, hipEventSynchronize(H.ev));
     }
     // the batch's landmark rows, packed on the device in frame order (k_lm_pack): one copy each
     // of X and keep into pinned memory (per-frame copies into pageable vectors cost ~2 x B
@@ -968,8 +989,8 @@ static int collect_batch(vo_ctx* c, vo_step_out* outs, int capacity, int* n_out)
     total = roff[B];
     if (c->lm_camera) {
         // camera-frame rows stay on the device: the tracked frames' packed rows are appended to
-        // the store by one device-to-device copy on `stream` (ordered before the next submit of
-        // this set, which reuses the packed buffer)
+        // the store by one device-to-device copy on `stream` (ordered before the next submit
+        // into this slot, which reuses the packed buffer: it needs this collect first)
         const size_t first = (P.first_tracked ? 0 : roff[1]), add = total - first;
         if (add > 0) {
             if (c->lm_n + add > c->lm_cap) {
@@ -980,28 +1001,30 @@ static int collect_batch(vo_ctx* c, vo_step_out* outs, int capacity, int* n_out)
                     hipFree(nX);
                     return fail(c, VO_ERR_HIP, "vo_step_collect: landmark store of %zu rows", cap);
                 }
-                // the store at least doubles, so this synchronising growth happens O(log rows) times
+                // the store at least doubles; the old one is copied on `stream` (in order with the
+                // appends) and retired until reset / destroy, so growth never waits for the pipeline
                 hipError_t ge = hipSuccess;
                 if (c->lm_n > 0) {
                     ge = hipMemcpyAsync(nX, c->d_lmX, sizeof(float) * 3 * c->lm_n, hipMemcpyDeviceToDevice, c->stream);
                     if (ge == hipSuccess) ge = hipMemcpyAsync(nk, c->d_lmkeep, c->lm_n, hipMemcpyDeviceToDevice, c->stream);
                 }
-                if (ge == hipSuccess) ge = hipStreamSynchronize(c->stream);
                 if (ge != hipSuccess) {
+                    (void)hipStreamSynchronize(c->stream);   // the copies may be queued: let them drain
                     hipFree(nX); hipFree(nk);
                     return fail(c, VO_ERR_HIP, "vo_step_collect: landmark store growth: %s", hipGetErrorString(ge));
                 }
-                hipFree(c->d_lmX); hipFree(c->d_lmkeep);
+                if (c->d_lmX) c->lm_retired.push_back(c->d_lmX);
+                if (c->d_lmkeep) c->lm_retired.push_back(c->d_lmkeep);
                 c->d_lmX = nX; c->d_lmkeep = nk; c->lm_cap = cap;
             }
-            HIPC(c, hipMemcpyAsync(c->d_lmX + 3 * c->lm_n, S.gb->lm_pX + 3 * first, sizeof(float) * 3 * add,
+            HIPC(c, hipMemcpyAsync(c->d_lmX + 3 * c->lm_n, H.d_pX + 3 * first, sizeof(float) * 3 * add,
                                    hipMemcpyDeviceToDevice, c->stream));
-            HIPC(c, hipMemcpyAsync(c->d_lmkeep + c->lm_n, S.gb->lm_pkeep + first, add, hipMemcpyDeviceToDevice, c->stream));
+            HIPC(c, hipMemcpyAsync(c->d_lmkeep + c->lm_n, H.d_pkeep + first, add, hipMemcpyDeviceToDevice, c->stream));
             c->lm_n += add;
         }
     } else if (total > 0) {
-        HIPC(c, hipMemcpyAsync(H.pX, S.gb->lm_pX, sizeof(float) * 3 * total, hipMemcpyDeviceToHost, c->copy_stream));
-        HIPC(c, hipMemcpyAsync(H.pkeep, S.gb->lm_pkeep, total, hipMemcpyDeviceToHost, c->copy_stream));
+        HIPC(c, hipMemcpyAsync(H.pX, H.d_pX, sizeof(float) * 3 * total, hipMemcpyDeviceToHost, c->copy_stream));
+        HIPC(c, hipMemcpyAsync(H.pkeep, H.d_pkeep, total, hipMemcpyDeviceToHost, c->copy_stream));
         HIPC(c, hipStreamSynchronize(c->copy_stream));
     }
     c->pending.pop_front();
@@ -1117,6 +1140,9 @@ int vo_fetch_tracks(vo_ctx* c, int frame, float* old_l, float* cur_l, double* wo
     if (!c || capacity < 0) return fail(c, VO_ERR_ARG, "vo_fetch_tracks: bad arguments");
     if (c->last_step_set < 0 || frame < 0 || frame >= c->last_step_B)
         return fail(c, VO_ERR_STATE, "vo_fetch_tracks: frame %d not in the last collected batch", frame);
+    for (const vo_ctx::Pending& q : c->pending)
+        if (q.set == c->last_step_set)
+            return fail(c, VO_ERR_STATE, "vo_fetch_tracks: the collected batch's buffer set is reused by a pending batch");
     hipSetDevice(c->device);
     SetRef S = set_ref(c, c->last_step_set);
     const int K = c->sb.kp_cap;
@@ -1267,6 +1293,9 @@ int vo_reset(vo_ctx* c)
     HIPC(c, hipStreamSynchronize(c->copy_stream));
     c->pending.clear();
     c->next_step_set = 0;
+    c->next_slot = 0;
+    for (void* p : c->lm_retired) hipFree(p);
+    c->lm_retired.clear();
     c->last_step_set = -1;
     c->have_features = false;
     c->frame_index = 0;

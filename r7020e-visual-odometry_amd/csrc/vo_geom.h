@@ -52,8 +52,6 @@ struct GeomBuffers {
     int* lm_rows = nullptr;      // [max_frames]
     // the batch's landmark rows packed in frame order (one D2H copy per batch): row r of frame f
     // at sum_{g<f} min(lm_rows[g], kp_cap) + r
-    float* lm_pX = nullptr;      // [max_frames * kp_cap][3]
-    uint8_t* lm_pkeep = nullptr; // [max_frames * kp_cap]
 };
 
 hipError_t geom_alloc(GeomBuffers& g, int max_frames, int kp_cap, int n_hyp);
@@ -85,8 +83,9 @@ void track_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_tra
                    const vo_match_params& mp, hipStream_t s);
 static inline int* track_list(const GeomBuffers& g, int f, int l) { return g.lists + ((size_t)f * TL_COUNT + l) * g.kp_cap; }
 
-// Pack frames [0, B)'s landmark rows contiguously into lm_pX / lm_pkeep.
-void lm_pack_launch(GeomBuffers& g, int B, hipStream_t s);
+// Pack frames [0, B)'s landmark rows contiguously into pX [B * kp_cap][3] / pkeep [B * kp_cap]
+// (the submitting batch's own buffers: they outlive the buffer set's reuse by the batch after next).
+void lm_pack_launch(GeomBuffers& g, int B, float* pX, uint8_t* pkeep, hipStream_t s);
 
 // CreateLandmarksFromFeatures.m:17 on the device for a run of frames: frame f's rows
 // [off[f], off[f+1]) of the camera-frame store (X [rows][3], keep [rows]) go to the world with

@@ -248,12 +248,17 @@ class KittiSequence:
         self._pool.shutdown(wait=True)
 
 
-def _pipelined(ctx, batches, dev, on_collect=None) -> list:
+def _pipelined(ctx, batches, dev, on_collect=None, depth: int | None = None) -> list:
     """Drive the loop body through vo_step_submit_dev / vo_step_collect: while batch n's
     kernels run, the host decodes and uploads batch n+1 (threaded PNG decode, pinned H2D),
-    and batch n+1's SIFT overlaps batch n's geometry.  Input tensors stay referenced until
-    their batch is collected."""
+    and batch n+1's SIFT overlaps batch n's geometry.  Up to `depth` batches are in flight
+    (default vo.STEP_DEPTH = 3, so batch n+2's scale space is queued before batch n's geometry
+    ends; 2 with `on_collect`, whose vo_fetch_tracks needs the collected batch's buffer set
+    intact).  Input tensors stay referenced until their batch is collected."""
     import torch
+    from . import vo
+    if depth is None:
+        depth = 2 if on_collect is not None else vo.STEP_DEPTH
     outs, inflight = [], []
 
     def collect():
@@ -277,7 +282,7 @@ def _pipelined(ctx, batches, dev, on_collect=None) -> list:
             torch.cuda.current_stream(dev).synchronize()     # inputs ready before the submit
         ctx.step_submit_dev(dl.data_ptr(), dr.data_ptr(), dl.shape[0])
         inflight.append((dl, dr, b0, L if on_collect is not None else None))
-        if ctx.steps_pending() == 2:
+        if ctx.steps_pending() == depth:
             collect()
     while ctx.steps_pending():
         collect()

@@ -35,6 +35,7 @@ VO_ERR_TOO_FEW_POINTS = -3
 VO_ERR_NO_CONSENSUS = -4
 VO_ERR_CAPACITY = -5
 VO_ERR_STATE = -6
+STEP_DEPTH = 3            # VO_STEP_DEPTH: batches vo_step_submit_dev keeps in flight
 
 
 class VOError(RuntimeError):

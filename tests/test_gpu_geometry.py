@@ -175,9 +175,12 @@ def test_sequence_stepwise_bit_exact(vo, oracle, syn, seq, calib):
     _compare_seq(outs2, ctx.get_landmarks(), routs, rlm)
 
 
-def test_sequence_pipelined_bit_exact(vo, oracle, syn, seq, calib):
-    """vo_step_submit_dev / vo_step_collect (two buffer sets, batch n+1's SIFT overlapping
-    batch n's geometry) give the oracle's VO.m loop bit for bit, with ragged batches."""
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_sequence_pipelined_bit_exact(vo, oracle, syn, seq, calib, depth):
+    """vo_step_submit_dev / vo_step_collect (two buffer sets, three result slots: batch n+1's
+    SIFT overlapping batch n's geometry, batch n+2's scale space queued before batch n's
+    geometry ends) give the oracle's VO.m loop bit for bit, with ragged batches, whether 1, 2
+    or 3 batches are kept in flight -- in the world-frame and the camera-frame landmark modes."""
     import torch
     L, R, _ = seq
     routs, rlm = oracle.run_sequence(L, R, syn.KITTI00_P0, syn.KITTI00_P1)
@@ -185,23 +188,36 @@ def test_sequence_pipelined_bit_exact(vo, oracle, syn, seq, calib):
     dl, dr = torch.from_numpy(np.ascontiguousarray(L)).cuda(), torch.from_numpy(np.ascontiguousarray(R)).cuda()
     torch.cuda.synchronize()
     fs = L[0].size
-    bounds = [(0, 2), (2, 3), (3, 6)]
-    outs = []
-    for k, (a, b) in enumerate(bounds):
-        ctx.step_submit_dev(dl.data_ptr() + a * fs, dr.data_ptr() + a * fs, b - a)
-        if k >= 1:
+    bounds = [(0, 2), (2, 3), (3, 4), (4, 6)]
+
+    def run():
+        outs = []
+        for a, b in bounds:
+            ctx.step_submit_dev(dl.data_ptr() + a * fs, dr.data_ptr() + a * fs, b - a)
+            if ctx.steps_pending() == depth:
+                outs.append(ctx.step_collect())
+        while ctx.steps_pending():
             outs.append(ctx.step_collect())
-    while ctx.steps_pending():
-        outs.append(ctx.step_collect())
-    _compare_seq(np.concatenate(outs), ctx.get_landmarks(), routs, rlm)
-    # pipeline rules: at most two batches pending, other calls refused meanwhile
+        return np.concatenate(outs)
+    _compare_seq(run(), ctx.get_landmarks(), routs, rlm)
+    # camera-frame rows kept on the device (the sharded path): the same rows, moved to the world
     ctx.reset()
-    ctx.step_submit_dev(dl.data_ptr(), dr.data_ptr(), 1)
-    ctx.step_submit_dev(dl.data_ptr() + fs, dr.data_ptr() + fs, 1)
+    ctx.set_landmark_frame(True)
+    outs = run()
+    X, keep = ctx.get_landmark_rows()
+    assert np.array_equal(vo.landmarks_to_world_frames(outs["pose"], outs["n_landmarks"], X, keep), rlm)
+    ctx.set_landmark_frame(False)
+    # pipeline rules: at most VO_STEP_DEPTH (3) batches pending, other calls refused meanwhile
+    ctx.reset()
+    for k in range(vo.STEP_DEPTH):
+        ctx.step_submit_dev(dl.data_ptr() + k * fs, dr.data_ptr() + k * fs, 1)
     with pytest.raises(vo.VOError):
-        ctx.step_submit_dev(dl.data_ptr() + 2 * fs, dr.data_ptr() + 2 * fs, 1)
+        ctx.step_submit_dev(dl.data_ptr() + 3 * fs, dr.data_ptr() + 3 * fs, 1)
     with pytest.raises(vo.VOError):
         ctx.step_batch_dev(dl.data_ptr(), dr.data_ptr(), 1)
+    ctx.step_collect()
+    with pytest.raises(vo.VOError):              # the collected batch's buffer set is in use again
+        ctx.fetch_tracks(0)
     ctx.step_collect()
     ctx.step_collect()
     with pytest.raises(vo.VOError):
