@@ -309,6 +309,10 @@ int vo_sift_match_batch_dev(vo_ctx* ctx, const uint8_t* d_lefts, const uint8_t* 
  * a frame.  Host output buffers. */
 int vo_fetch_keypoints(vo_ctx* ctx, int image, vo_keypoint* kps, uint8_t* desc, int capacity, int* n);
 int vo_fetch_stereo_pairs(vo_ctx* ctx, int frame, uint32_t* pairs, int capacity, int* n);
+/* Extremum candidates of image i in the last batched call (uncapped: above 4 x max_keypoints
+ * the list was truncated, VO_FLAG_CANDIDATES) and how many passed refinement (contrast, edge
+ * and the outer-level extremum test) -- the counts the feature kernels' byte model prices. */
+int vo_fetch_candidate_counts(vo_ctx* ctx, int image, int* n_cand, int* n_accepted);
 /* Gaussian scale-space level G(octave, level) of image i from the last batched
  * call (rows x cols floats, tightly packed; out == NULL only reports the size).
  * Diagnostic: the scale space has no MATLAB counterpart (detectSIFTFeatures

@@ -811,6 +811,21 @@ int vo_fetch_keypoints(vo_ctx* c, int image, vo_keypoint* kps, uint8_t* desc, in
     return VO_OK;
 }
 
+int vo_fetch_candidate_counts(vo_ctx* c, int image, int* n_cand, int* n_accepted)
+{
+    if (!c || image < 0 || image >= c->sb.n_img) return fail(c, VO_ERR_ARG, "vo_fetch_candidate_counts: bad image");
+    hipSetDevice(c->device);
+    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipEventSynchronize(c->ev_done[c->last_set]));
+    const SiftBuffers& B = (c->last_set == 1 && image < 2 * c->max_batch) ? c->aux.sb : c->sb;
+    int v[2] = {0, 0};
+    HIPC(c, hipMemcpy(&v[0], B.n_cand + image, sizeof(int), hipMemcpyDeviceToHost));
+    HIPC(c, hipMemcpy(&v[1], B.n_acc + image, sizeof(int), hipMemcpyDeviceToHost));
+    if (n_cand) *n_cand = v[0];
+    if (n_accepted) *n_accepted = v[1];
+    return VO_OK;
+}
+
 int vo_fetch_gaussian(vo_ctx* c, int image, int octave, int level, float* out, int capacity, int* rows, int* cols)
 {
     if (!c || image < 0 || image >= c->sb.n_img || octave < 0 || octave >= c->py.n_oct || level < 0 ||

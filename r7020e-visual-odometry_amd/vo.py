@@ -94,6 +94,7 @@ EXPORTS = [
     "vo_kernel_times", "vo_set_frame_index", "vo_set_concurrency",
     "vo_set_landmark_frame", "vo_get_landmark_rows", "vo_landmarks_to_world", "vo_match_f32",
     "vo_sift_ex", "vo_step_batch_ex", "vo_chain_poses", "vo_landmarks_to_world_frames", "vo_landmarks_world_dev",
+    "vo_fetch_candidate_counts",
 ]
 
 # the test build (csrc `make exp`, -DVO_EXPERIMENTAL=1): libvo plus the experimental kernels kept
@@ -162,6 +163,7 @@ def load_library(path: str | os.PathLike | None = None):
     L.vo_sift_match_batch_dev.argtypes = [vp, vp, vp, C.c_int, P(PairStats)]
     L.vo_fetch_keypoints.argtypes = [vp, C.c_int, P(Keypoint), P(C.c_uint8), C.c_int, P(C.c_int)]
     L.vo_fetch_stereo_pairs.argtypes = [vp, C.c_int, P(C.c_uint32), C.c_int, P(C.c_int)]
+    L.vo_fetch_candidate_counts.argtypes = [vp, C.c_int, P(C.c_int), P(C.c_int)]
     L.vo_fetch_gaussian.argtypes = [vp, C.c_int, C.c_int, C.c_int, P(C.c_float), C.c_int, P(C.c_int), P(C.c_int)]
     L.vo_stream.argtypes = [vp]
     L.vo_stream.restype = vp
@@ -341,6 +343,13 @@ class Context:
                                                 _p(desc, C.c_uint8), cap, C.byref(n)))
         m = min(n.value, cap)
         return kps[:m].copy(), desc[:m].copy()
+
+    def fetch_candidate_counts(self, image: int) -> tuple[int, int]:
+        """(extremum candidates, candidates accepted by the refinement) of `image` in the last
+        batched call (vo_fetch_candidate_counts)."""
+        nc, na = C.c_int(0), C.c_int(0)
+        self._check(self.lib.vo_fetch_candidate_counts(self.h, image, C.byref(nc), C.byref(na)))
+        return nc.value, na.value
 
     def fetch_stereo_pairs(self, frame: int) -> np.ndarray:
         cap = self.sift_params.max_keypoints

@@ -91,6 +91,21 @@ for st in $STEPS; do
     python3 tools/stream_busy.py $(find $O/strace -name "*kernel_trace.csv" | head -1) > $O/stream_busy.txt
     find $O/strace -name "*.csv" -delete
     cat $O/stream_busy.txt ;;
+  seqbusy:*)
+    # seqbusy:<frames>:<batch>:<depth>:<skip> -- per-stream occupancy of the full path's pipelined loop
+    a=${st#seqbusy:}; IFS=: read -r n b d k <<< "$a"
+    timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/sq_${b}_${d} -o t -- python3 tools/seq_run.py $n $b $d > $O/sq_${b}_$d.log 2>&1 \
+      || { tail -20 $O/sq_${b}_$d.log; exit 1; }
+    python3 tools/stream_busy.py $(find $O/sq_${b}_${d} -name "*kernel_trace.csv" | head -1) $k > $O/stream_busy_seq_${b}_$d.txt
+    find $O/sq_${b}_${d} -name "*.csv" -delete
+    grep pass $O/sq_${b}_$d.log; cat $O/stream_busy_seq_${b}_$d.txt ;;
+  fcalib)
+    # FETCH_SIZE calibration for the feature kernels' access shapes (tools/fetch_calib.hip)
+    timeout -s KILL 90 rocprofv3 --kernel-trace --output-format csv -d $O/fcal -o f --pmc FETCH_SIZE -- ./tools/fetch_calib > $O/fetch_calib.txt 2>&1 \
+      || { tail -20 $O/fetch_calib.txt; exit 1; }
+    python3 tools/fetch_calib_sum.py $(find $O/fcal -name "*counter_collection.csv" | head -1) $O/fetch_calib.txt > $O/fetch_calib_sum.txt
+    find $O/fcal -name "*.csv" -delete
+    cat $O/fetch_calib_sum.txt ;;
   insitu)
     # kernel trace of the asynchronous loop + the counter passes -> tools/insitu_model.py
     timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $O/itrace -o t -- python3 tools/prof_run.py ${PMC_BATCH:-256} 6 > $O/itrace.log 2>&1 \
