@@ -943,6 +943,17 @@ void track_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_tra
                    const vo_match_params& mp, hipStream_t s)
 {
     const int B = a.B, M = a.max_frames, K = a.kp_cap;
+#ifndef VO_TRACK_FUSED
+#define VO_TRACK_FUSED 1          // 0: the unfused chain (4 x match partial / merge / compact + k_compose)
+#endif
+    if (VO_TRACK_FUSED) {
+        TrackArgs ta;
+        ta.jobs = d_track_jobs; ta.M = M; ta.kp_cap = K; ta.row_cap = mb.row_cap;
+        ta.lists = g.lists; ta.list_n = g.list_n; ta.pair_i = a.pair_i; ta.pair_j = a.pair_j;
+        ta.res = mb.res; ta.T = mp.match_threshold * 0.04f; ta.max_ratio = mp.max_ratio;
+        track_fused_launch(ta, B, s);
+        return;
+    }
     ComposeArgs ca;
     ca.lists = g.lists; ca.list_n = g.list_n; ca.step_i = g.step_i; ca.step_j = g.step_j; ca.step_n = g.step_n;
     ca.pair_i = a.pair_i; ca.pair_j = a.pair_j; ca.pair_n = a.pair_n; ca.M = M; ca.kp_cap = K;

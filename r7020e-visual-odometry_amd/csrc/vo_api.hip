@@ -276,14 +276,7 @@ vo_ctx* vo_create(int device, int rows, int cols, int max_batch, const vo_calib*
         return nullptr;
     };
     hipError_t e;
-#ifndef VO_GEOM_PRIO
-#define VO_GEOM_PRIO 0            // 1: the geometry stream (`stream`) at the device's highest priority
-#endif
-    if (VO_GEOM_PRIO) {
-        int lo = 0, hi = 0;
-        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        if ((e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi)) != hipSuccess) return bail("stream", e);
-    } else if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bail("stream", e);
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bail("stream", e);
     for (int k = 0; k < vo_ctx::MAX_SUB; ++k) {
         // every stream at the default priority: the forked SIFT streams must not rank below the
         // geometry / copy streams of the pipelined loop body (at the lowest priority the full

@@ -78,6 +78,19 @@ struct StepArgs {
 // landmark kernels for frames [0, B).  match jobs at d_jobs + first.
 void geom_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_track_jobs, const StepArgs& a,
                   const vo_match_params& mp, hipStream_t s);
+// find_remaining_points fused (VO.m:283-333): one workgroup per frame runs the frame's four
+// dependent matches, each followed by its compaction in ascending F1 order and its index
+// composition, in one launch (csrc/match.hip k_track).  jobs: the track jobs (step s of frame f
+// at jobs[s * M + f]); res: per-frame scratch rows [B][row_cap].
+struct TrackArgs {
+    const MatchJob* jobs;
+    int M, kp_cap, row_cap;
+    int* lists; int* list_n;
+    const int* pair_i; const int* pair_j;     // stereo pairs per pair slot (frame f-1's, or slot M)
+    int* res;
+    float T, max_ratio;
+};
+void track_fused_launch(const TrackArgs& a, int B, hipStream_t s);
 // tracking only (4 matches + compositions); lists/list_n valid afterwards.
 void track_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_track_jobs, const StepArgs& a,
                    const vo_match_params& mp, hipStream_t s);
