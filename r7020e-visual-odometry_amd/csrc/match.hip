@@ -437,99 +437,111 @@ __device__ __forceinline__ uint32_t block_exscan_256(uint32_t v, uint32_t* sh, u
     return before + x - v;
 }
 
-// find_remaining_points (VO.m:283-333) for one frame per workgroup: its four dependent
-// matchFeatures calls (lm, rm, cm, last), each
-//   (1) every F1 row against all F2 columns, 128 rows at a time (mp_block, the whole column
-//       range as one chunk: the same exact top-2 k_match_partial + k_match_merge reach over
-//       chunks, since the merge is an order-free (value, index) rule), MatchThreshold and
-//       MaxRatio applied in place (k_match_merge's test) -> res[row];
-//   (2) the accepted rows compacted in ascending F1 order (k_match_compact's rule);
-//   (3) the index composition of VO.m:287-290 / 297-308 / 314-317 / 326-333 (k_compose).
-// Each step's row counts come from the previous step's composition in this workgroup, so the
-// 16 dependent launches of the unfused chain (and their grid-wide drains) become one.
-__global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_track(TrackArgs a)
+// One step s of find_remaining_points (VO.m:283-333: lm, rm, cm, last) for every frame of the
+// batch: grid (W, B), workgroup (x, f) takes F1 row blocks x, x + W, ... of frame f's step-s
+// match and
+//   (1) matches them against all F2 columns (mp_block over the whole column range as one
+//       chunk: the same exact top-2 that k_match_partial + k_match_merge reach over chunks,
+//       since the merge is an order-free (value, index) rule) and applies MatchThreshold and
+//       MaxRatio in place (k_match_merge's test) -> res[row];
+// the frame's last workgroup to finish (a per-frame counter; no workgroup ever waits) then
+//   (2) compacts the accepted rows in ascending F1 order (k_match_compact's rule) and
+//   (3) composes the index lists (k_compose; VO.m:287-290 / 297-308 / 314-317 / 326-333).
+// So each step is one launch instead of four (partial, merge, compact, compose), and the next
+// step's row counts are the list lengths this one leaves.
+__global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_track_step(TrackArgs a, int s)
 {
     __shared__ __attribute__((aligned(16))) MpTiles T;
     __shared__ uint32_t wsum[4];
-    const int f = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l31 = lane & 31;
+    __shared__ int s_last;
+    const int x = blockIdx.x, W = gridDim.x, f = blockIdx.y;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l31 = lane & 31;
     const int K = a.kp_cap, M = a.M;
-    int* L = a.lists + (size_t)f * TL_COUNT * K;
     int* res = a.res + (size_t)f * a.row_cap;
-    const int pp = f ? f - 1 : M;
-    for (int s = 0; s < 4; ++s) {
-        const MatchJob J = a.jobs[s * M + f];
-        const int n1 = job_rows(J.n1, a.row_cap), n2 = job_rows(J.n2, a.row_cap);
-        if (n2 == 0) {
-            for (int r = tid; r < n1; r += 256) res[r] = -1;
-        } else {
-            for (int i0b = 0; i0b < n1; i0b += MP_ROWS) {
-                float best[16], second[16];
-                int bidx[16];
-                mp_block(J, n1, i0b, 0, n2, T, best, bidx, second);
-                if (l31 < 16) {
-                    float bb, ss;
-                    int ii;
-                    mp_row_result(l31, best, bidx, second, bb, ii, ss);
-                    const int row = mp_lane_row(i0b + 32 * wave, l31, h);
-                    if (row < n1) {
-                        float b = -INFINITY, sv = -INFINITY;
-                        int i = -1;
-                        top2c_merge(b, i, sv, bb, ii, ss);          // k_match_merge over one chunk
-                        const float bs = 2.0f - 2.0f * b, ssd2 = 2.0f - 2.0f * sv;
-                        res[row] = (i >= 0 && bs <= a.T && (bs / ssd2) <= a.max_ratio) ? i : -1;
-                    }
+    const MatchJob J = a.jobs[s * M + f];
+    const int n1 = job_rows(J.n1, a.row_cap), n2 = job_rows(J.n2, a.row_cap);
+    if (n2 == 0) {
+        for (int r = x * 256 + tid; r < n1; r += W * 256) res[r] = -1;
+    } else {
+        for (int i0b = x * MP_ROWS; i0b < n1; i0b += W * MP_ROWS) {      // workgroup-uniform
+            float best[16], second[16];
+            int bidx[16];
+            mp_block(J, n1, i0b, 0, n2, T, best, bidx, second);
+            if (l31 < 16) {
+                float bb, ss;
+                int ii;
+                mp_row_result(l31, best, bidx, second, bb, ii, ss);
+                const int row = mp_lane_row(i0b + 32 * wave, l31, h);
+                if (row < n1) {
+                    float b = -INFINITY, sv = -INFINITY;
+                    int i = -1;
+                    top2c_merge(b, i, sv, bb, ii, ss);          // k_match_merge over one chunk
+                    const float bs = 2.0f - 2.0f * b, ssd2 = 2.0f - 2.0f * sv;
+                    res[row] = (i >= 0 && bs <= a.T && (bs / ssd2) <= a.max_ratio) ? i : -1;
                 }
             }
         }
-        __syncthreads();
-        // accepted rows in ascending F1 order
-        const int chunk = (n1 + 255) / 256;
-        const int r0 = min(tid * chunk, n1), r1 = min(r0 + chunk, n1);
-        uint32_t cnt = 0;
-        for (int r = r0; r < r1; ++r) cnt += res[r] >= 0;
-        uint32_t total;
-        uint32_t base = block_exscan_256(cnt, wsum, &total);
-        for (int r = r0; r < r1; ++r) {
-            const int i = res[r];
-            if (i >= 0) {
-                if (base < (uint32_t)J.cap) { gst(J.out_i + base, r); gst(J.out_j + base, i); }
-                base++;
-            }
-        }
-        const int n_out = (int)(total < (uint32_t)J.cap ? total : (uint32_t)J.cap);
-        if (tid == 0) gst(J.out_n, n_out);
-        __syncthreads();
-        // index composition (k_compose)
-        const int n = min(n_out, K);
-        for (int k = tid; k < n; k += 256) {
-            const int i = gld(J.out_i + k), j = gld(J.out_j + k);
-            if (s == 0) {
-                L[TL_OL1 * K + k] = a.pair_i[(size_t)pp * K + j];
-                L[TL_OR1 * K + k] = a.pair_j[(size_t)pp * K + j];
-                L[TL_CL * K + k] = i;
-            } else if (s == 1) {
-                L[TL_OL2 * K + k] = L[TL_OL1 * K + j];
-                L[TL_OR2 * K + k] = L[TL_OR1 * K + j];
-                L[TL_CR * K + k] = i;
-            } else if (s == 2) {
-                L[TL_CL2 * K + k] = L[TL_CL * K + i];
-                L[TL_CR2 * K + k] = L[TL_CR * K + j];
-            } else {
-                L[TL_OLF * K + k] = L[TL_OL2 * K + j];
-                L[TL_ORF * K + k] = L[TL_OR2 * K + j];
-                L[TL_CLF * K + k] = L[TL_CL2 * K + i];
-                L[TL_CRF * K + k] = L[TL_CR2 * K + i];
-            }
-        }
-        if (tid == 0) a.list_n[4 * f + s] = n;
-        __syncthreads();
     }
+    // release this workgroup's rows (device scope: the other workgroups may sit on other XCDs);
+    // the W-th arrival goes on, with an acquire before it reads any row
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) s_last = atomicAdd(a.cnt + f, 1) == W - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    // accepted rows in ascending F1 order
+    const int chunk = (n1 + 255) / 256;
+    const int r0 = min(tid * chunk, n1), r1 = min(r0 + chunk, n1);
+    uint32_t cnt = 0;
+    for (int r = r0; r < r1; ++r) cnt += __hip_atomic_load(res + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 0;
+    uint32_t total;
+    uint32_t base = block_exscan_256(cnt, wsum, &total);
+    for (int r = r0; r < r1; ++r) {
+        const int i = __hip_atomic_load(res + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (i >= 0) {
+            if (base < (uint32_t)J.cap) { gst(J.out_i + base, r); gst(J.out_j + base, i); }
+            base++;
+        }
+    }
+    const int n_out = (int)(total < (uint32_t)J.cap ? total : (uint32_t)J.cap);
+    if (tid == 0) { gst(J.out_n, n_out); a.cnt[f] = 0; }      // the counter is ready for the next step
+    __syncthreads();
+    // index composition (k_compose)
+    int* L = a.lists + (size_t)f * TL_COUNT * K;
+    const int pp = f ? f - 1 : M;
+    const int n = min(n_out, K);
+    for (int k = tid; k < n; k += 256) {
+        const int i = gld(J.out_i + k), j = gld(J.out_j + k);
+        if (s == 0) {
+            L[TL_OL1 * K + k] = a.pair_i[(size_t)pp * K + j];
+            L[TL_OR1 * K + k] = a.pair_j[(size_t)pp * K + j];
+            L[TL_CL * K + k] = i;
+        } else if (s == 1) {
+            L[TL_OL2 * K + k] = L[TL_OL1 * K + j];
+            L[TL_OR2 * K + k] = L[TL_OR1 * K + j];
+            L[TL_CR * K + k] = i;
+        } else if (s == 2) {
+            L[TL_CL2 * K + k] = L[TL_CL * K + i];
+            L[TL_CR2 * K + k] = L[TL_CR * K + j];
+        } else {
+            L[TL_OLF * K + k] = L[TL_OL2 * K + j];
+            L[TL_ORF * K + k] = L[TL_OR2 * K + j];
+            L[TL_CLF * K + k] = L[TL_CL2 * K + i];
+            L[TL_CRF * K + k] = L[TL_CR2 * K + i];
+        }
+    }
+    if (tid == 0) a.list_n[4 * f + s] = n;
 }
 
+#ifndef VO_TRACK_W
+#define VO_TRACK_W 8              // workgroups per frame and step (row blocks of 128 F1 rows each)
+#endif
 void track_fused_launch(const TrackArgs& a, int B, hipStream_t s)
 {
     if (B <= 0) return;
-    VO_LAUNCH(k_track, dim3(B), dim3(256), 0, s, a);
+    for (int step = 0; step < 4; ++step)
+        VO_LAUNCH(k_track_step, dim3(VO_TRACK_W, B), dim3(256), 0, s, a, step);
 }
 
 // Descriptor metadata for externally supplied descriptors (vo_match on host data).
