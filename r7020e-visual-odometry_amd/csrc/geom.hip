@@ -49,10 +49,7 @@ hipError_t geom_alloc(GeomBuffers& g, int max_frames, int kp_cap, int n_hyp)
     GA(g.lm_X, sizeof(float) * F * K * 3);
     GA(g.lm_keep, F * K);
     GA(g.lm_rows, sizeof(int) * F);
-    GA(g.track_cnt, sizeof(int) * F);
 #undef GA
-    e = hipMemset(g.track_cnt, 0, sizeof(int) * F);
-    if (e != hipSuccess) return e;
     e = hipMemset(g.step_n, 0, sizeof(int) * 4 * F);
     if (e != hipSuccess) return e;
     return hipMemset(g.list_n, 0, sizeof(int) * 4 * F);
@@ -61,7 +58,7 @@ hipError_t geom_alloc(GeomBuffers& g, int max_frames, int kp_cap, int n_hyp)
 void geom_free(GeomBuffers& g)
 {
     void* bufs[] = {g.lists, g.list_n, g.step_i, g.step_j, g.step_n, g.world, g.imgpt, g.oldpos, g.inliers, g.hyp,
-                    g.fg, g.spos, g.s_n, g.lm_new, g.lm_M, g.lm_X, g.lm_keep, g.lm_rows, g.track_cnt};
+                    g.fg, g.spos, g.s_n, g.lm_new, g.lm_M, g.lm_X, g.lm_keep, g.lm_rows};
     for (void* p : bufs) (void)hipFree(p);   // teardown: nothing to report to
     g = GeomBuffers();
 }
@@ -946,17 +943,6 @@ void track_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_tra
                    const vo_match_params& mp, hipStream_t s)
 {
     const int B = a.B, M = a.max_frames, K = a.kp_cap;
-#ifndef VO_TRACK_FUSED
-#define VO_TRACK_FUSED 1          // 0: the unfused chain (4 x match partial / merge / compact + k_compose)
-#endif
-    if (VO_TRACK_FUSED) {
-        TrackArgs ta;
-        ta.jobs = d_track_jobs; ta.M = M; ta.kp_cap = K; ta.row_cap = mb.row_cap;
-        ta.lists = g.lists; ta.list_n = g.list_n; ta.pair_i = a.pair_i; ta.pair_j = a.pair_j;
-        ta.res = mb.res; ta.cnt = g.track_cnt; ta.T = mp.match_threshold * 0.04f; ta.max_ratio = mp.max_ratio;
-        track_fused_launch(ta, B, s);
-        return;
-    }
     ComposeArgs ca;
     ca.lists = g.lists; ca.list_n = g.list_n; ca.step_i = g.step_i; ca.step_j = g.step_j; ca.step_n = g.step_n;
     ca.pair_i = a.pair_i; ca.pair_j = a.pair_j; ca.pair_n = a.pair_n; ca.M = M; ca.kp_cap = K;

@@ -14,7 +14,6 @@
 // MaxRatio; k_match_compact writes the pairs in ascending F1 order with a block
 // prefix sum.
 #include "vo_internal.h"
-#include "vo_geom.h"
 
 namespace vo {
 
@@ -139,164 +138,16 @@ __device__ __forceinline__ v4i load_frag(const uint8_t* row, int off)
 #ifndef VO_MP_BLOCKS
 #define VO_MP_BLOCKS 3            // workgroups per CU the register budget is sized for
 #endif
-
-// The F2 tile staging of one workgroup: rows padded to 144 B (36 dwords) -- the 32 lanes of a
-// half read 16 B at row l31, so a 128-B stride would put them all on the same banks.
-struct MpTiles {
-    uint8_t bt[2][32 * MP_LDS_ROW];
-    int bck[2][32];
-    float binb[2][32];
-};
-
-// One 128-row block of F1 (wave w: rows i0b + 32 w + [0, 32)) against F2 columns [j0, j1)
-// (j0 < j1) of job J, by the whole 256-thread workgroup.  On return every lane holds, for its
-// 16 accumulator rows, the top-2 in the cosine domain over the block's columns, merged over the
-// 32 lanes of its half: lane l31 < 16 of half h owns row i0b + 32 w + (l31 & 3) + 8 (l31 >> 2) + 4 h
-// (mp_lane_row).  Starts with a barrier (the previous block's readers of `T` are done).
-__device__ __forceinline__ int mp_lane_row(int i0, int l31, int h) { return i0 + (l31 & 3) + 8 * (l31 >> 2) + 4 * h; }
-
-__device__ __forceinline__ void mp_block(const MatchJob& J, int n1, int i0b, int j0, int j1, MpTiles& T,
-                                         float (&best)[16], int (&bidx)[16], float (&second)[16])
-{
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l31 = lane & 31;
-    const int lr = tid >> 3, lseg = tid & 7;              // loader: row lr of the tile, bytes [16 lseg, +16)
-    const int i0 = i0b + 32 * wave;
-    // A fragments: F1 row i0 + l31, bytes [32kk + 16h, +16)
-    v4i a[4];
-    {
-        const int ia = i0 + l31;
-        if (ia < n1) {
-            const int ra = J.idx1 ? gld(J.idx1 + ia) : ia;
-            const uint8_t* row = J.d1 + (size_t)ra * VO_DESC_LEN;
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) a[kk] = load_frag(row, 32 * kk + 16 * h);
-        } else {
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) a[kk] = (v4i){0, 0, 0, 0};
-        }
-    }
-    int rk[16];
-    float ina[16];
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-        const int row = mp_lane_row(i0, reg, h);
-        int sa = 0;
-        ina[reg] = 0.0f;
-        if (row < n1) {
-            const int ra = J.idx1 ? gld(J.idx1 + row) : row;
-            const DescMeta m = gld_meta(J.m1 + ra);
-            sa = m.sum; ina[reg] = m.inv_norm;
-        }
-        rk[reg] = 128 * sa - 2097152;
-        best[reg] = -INFINITY; second[reg] = -INFINITY; bidx[reg] = -1;
-    }
-    // loader: column jt + lr (clamped into the range; the epilogue masks columns >= j1)
-    v4i gv;
-    DescMeta gm;
-    auto gload = [&](int jt) {
-        const int jc = min(jt + lr, j1 - 1);
-        const int rb = J.idx2 ? gld(J.idx2 + jc) : jc;
-        gv = gld(reinterpret_cast<const v4i*>(J.d2 + (size_t)rb * VO_DESC_LEN + 16 * lseg));
-        if (lseg == 0) gm = gld_meta(J.m2 + rb);
-    };
-    // After tiles 1, 2, 4, 8, ... of the range every lane's second best of a row is raised
-    // to the max over the 32 lanes of the half (the row's wave-wide second best so far).
-    // The merged top-2 is unchanged: each lane's second is a candidate value other than
-    // its own best, so every second (raised or not) is <= the row's true second, which
-    // the merge still finds.  A value <= the raised second can never enter the row's final
-    // top-2 (later columns only lose ties), so the wave skips the update unless some lane
-    // beats its second -- rare once the row has settled.
-    int tno = 0;
-    auto lstore = [&](int buf) {                       // stored as b - 128 (the MFMA operand)
-        *reinterpret_cast<v4i*>(&T.bt[buf][lr * MP_LDS_ROW + 16 * lseg]) =
-            gv ^ (v4i){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
-        if (lseg == 0) { T.bck[buf][lr] = 128 * gm.sum; T.binb[buf][lr] = gm.inv_norm; }
-    };
-    gload(j0);
-    __syncthreads();                                   // previous block's readers are done with T
-    lstore(0);
-    if (j0 + 32 < j1) gload(j0 + 32);
-    int buf = 0;
-    for (int jt = j0; jt < j1; jt += 32, buf ^= 1) {
-        __syncthreads();                               // tile jt visible; tile jt-32's buffer free
-        if (jt + 32 < j1) {
-            lstore(buf ^ 1);                           // tile jt+32 (loaded one iteration ago)
-#if !(defined(VO_MATCH_DIAG) && VO_MATCH_DIAG == 2)
-            if (jt + 64 < j1) gload(jt + 64);          // (diagnostic build 2: no F2 loads after the first)
-#endif
-        }
-        v4i b[4];
-        const uint8_t* brow = &T.bt[buf][l31 * MP_LDS_ROW + 16 * h];
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) b[kk] = *reinterpret_cast<const v4i*>(brow + 32 * kk);
-        const int ck = T.bck[buf][l31];
-        const float inb = T.binb[buf][l31];
-        v16i accv = (v16i){0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) accv = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kk], b[kk], accv, 0, 0, 0);
-        const int jc = jt + l31;
-        // ragged last tile: masked columns get c = -inf (never ranked); elsewhere c + 0 = c
-        // exactly (c >= +0)
-        const float cmask = jc < j1 ? 0.0f : -INFINITY;
-#if defined(VO_MATCH_DIAG) && VO_MATCH_DIAG == 1
-        // diagnostic build 1 (timing only): no epilogue, the accumulators feed one running max
-        for (int reg = 0; reg < 16; ++reg) best[reg] = fmaxf(best[reg], (float)accv[reg] + cmask);
-#else
-#pragma unroll
-        for (int reg = 0; reg < 16; reg += 2) {
-            // c for two accumulator rows at once: the two products as packed f32 muls
-            // (each component an IEEE multiply, same bits as the scalar form)
-            const vo_f2 fp = vo_f2{(float)(accv[reg] + rk[reg] + ck), (float)(accv[reg + 1] + rk[reg + 1] + ck)};
-            vo_f2 cp = (fp * vo_f2{ina[reg], ina[reg + 1]}) * vo_f2{inb, inb};
-            cp = cp + vo_f2{cmask, cmask};
-#pragma unroll
-            for (int h2 = 0; h2 < 2; ++h2) {
-                const int q = reg + h2;
-                const float c = h2 ? cp.y : cp.x;
-                if (__builtin_amdgcn_ballot_w64(c > second[q])) {
-                    const bool g1 = c > best[q], g2 = c > second[q];
-                    second[q] = g1 ? best[q] : (g2 ? c : second[q]);
-                    best[q] = g1 ? c : best[q];
-                    bidx[q] = g1 ? jc : bidx[q];
-                }
-            }
-        }
-#endif
-        ++tno;
-        if ((tno & (tno - 1)) == 0) {                  // wave-uniform
-#pragma unroll
-            for (int reg = 0; reg < 16; ++reg) second[reg] = half_max(second[reg]);
-        }
-    }
-    // merge the 32 lanes of each half (same accumulator rows, different columns)
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) half_top2c(best[reg], bidx[reg], second[reg]);
-}
-
-// The merged top-2 of accumulator row `l31` (lanes l31 < 16; select by unrolled compare).
-__device__ __forceinline__ void mp_row_result(int l31, const float (&best)[16], const int (&bidx)[16],
-                                              const float (&second)[16], float& bb, int& ii, float& ss)
-{
-    bb = -INFINITY; ss = -INFINITY; ii = -1;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg)
-        if (reg == l31) { bb = best[reg]; ii = bidx[reg]; ss = second[reg]; }
-}
-
-// One workgroup (4 waves) per (job, 128-row F1 block, CHUNK-column F2 chunk); wave w owns
-// F1 rows [128 blk + 32 w, +32).  The F2 side is shared: each 32-column tile (4 KB of
-// descriptors + metadata) is loaded once per workgroup, one 16-B load per thread, staged
-// through a double-buffered LDS tile, and read by every wave as MFMA B fragments.  Tile t+1
-// is written to LDS and tile t+2 is in flight from HBM/L2 while tile t runs its 4 MFMAs
-// and epilogue.  Epilogue per accumulator element: dot = acc + 128 sa - 2^21 + 128 sb (one
-// add3), c = ((float)dot * inv|a|) * inv|b| (packed muls, two rows at once), then the top-2
-// update, skipped by the wave when no lane's c beats its row's second best.  The half-wave
-// reductions (second-best refresh, final merge) use DPP rotations and v_permlane16_swap.
 __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const MatchJob* __restrict__ jobs, int n_jobs,
                                                        MatchTop2* __restrict__ partial, int row_cap, int n_chunks_cap)
 {
-    __shared__ __attribute__((aligned(16))) MpTiles T;
+    // F2 tile rows padded to 144 B (36 dwords): the 32 lanes of a half read 16 B at row l31,
+    // so a 128-B stride would put them all on the same banks
+    __shared__ __attribute__((aligned(16))) uint8_t bt[2][32 * MP_LDS_ROW];
+    __shared__ int bck[2][32];
+    __shared__ float binb[2][32];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l31 = lane & 31;
+    const int lr = tid >> 3, lseg = tid & 7;              // loader: row lr of the tile, bytes [16 lseg, +16)
     // task table: job j owns tasks [tstart[j], tstart[j+1]); job sizes are read on device
     // (counts of earlier kernels), one thread per job, then a block prefix sum
     __shared__ int tstart[VO_MP_MAX_JOBS + 1], jn1[VO_MP_MAX_JOBS], jnch[VO_MP_MAX_JOBS];
@@ -329,15 +180,128 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
         const long rel = t - tstart[jb];
         const MatchJob J = jobs[jb];
         const int blk = (int)(rel / nch), chunk = (int)(rel - (long)blk * nch);
-        const int j0 = chunk * VO_MATCH_CHUNK, j1 = min(j0 + VO_MATCH_CHUNK, n2);
+        const int i0 = blk * MP_ROWS + 32 * wave, j0 = chunk * VO_MATCH_CHUNK;
+        const int j1 = min(j0 + VO_MATCH_CHUNK, n2);
+        // A fragments: F1 row i0 + l31, bytes [32kk + 16h, +16)
+        v4i a[4];
+        {
+            const int ia = i0 + l31;
+            if (ia < n1) {
+                const int ra = J.idx1 ? gld(J.idx1 + ia) : ia;
+                const uint8_t* row = J.d1 + (size_t)ra * VO_DESC_LEN;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) a[kk] = load_frag(row, 32 * kk + 16 * h);
+            } else {
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) a[kk] = (v4i){0, 0, 0, 0};
+            }
+        }
+        int rk[16];
+        float ina[16];
         float best[16], second[16];
         int bidx[16];
-        mp_block(J, n1, blk * MP_ROWS, j0, j1, T, best, bidx, second);
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int row = i0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            int sa = 0;
+            ina[reg] = 0.0f;
+            if (row < n1) {
+                const int ra = J.idx1 ? gld(J.idx1 + row) : row;
+                const DescMeta m = gld_meta(J.m1 + ra);
+                sa = m.sum; ina[reg] = m.inv_norm;
+            }
+            rk[reg] = 128 * sa - 2097152;
+            best[reg] = -INFINITY; second[reg] = -INFINITY; bidx[reg] = -1;
+        }
+        // loader: column jt + lr (clamped into the chunk; the epilogue masks columns >= j1)
+        v4i gv;
+        DescMeta gm;
+        auto gload = [&](int jt) {
+            const int jc = min(jt + lr, j1 - 1);
+            const int rb = J.idx2 ? gld(J.idx2 + jc) : jc;
+            gv = gld(reinterpret_cast<const v4i*>(J.d2 + (size_t)rb * VO_DESC_LEN + 16 * lseg));
+            if (lseg == 0) gm = gld_meta(J.m2 + rb);
+        };
+        // After tiles 1, 2, 4, 8, ... of the chunk every lane's second best of a row is raised
+        // to the max over the 32 lanes of the half (the row's wave-wide second best so far).
+        // The merged top-2 is unchanged: each lane's second is a candidate value other than
+        // its own best, so every second (raised or not) is <= the row's true second, which
+        // the merge still finds.  A value <= the raised second can never enter the row's final
+        // top-2 (later columns only lose ties), so the wave skips the update unless some lane
+        // beats its second -- rare once the row has settled.
+        int tno = 0;
+        auto lstore = [&](int buf) {                       // stored as b - 128 (the MFMA operand)
+            *reinterpret_cast<v4i*>(&bt[buf][lr * MP_LDS_ROW + 16 * lseg]) =
+                gv ^ (v4i){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
+            if (lseg == 0) { bck[buf][lr] = 128 * gm.sum; binb[buf][lr] = gm.inv_norm; }
+        };
+        gload(j0);
+        __syncthreads();                                   // previous task's readers are done with bt
+        lstore(0);
+        if (j0 + 32 < j1) gload(j0 + 32);
+        int buf = 0;
+        for (int jt = j0; jt < j1; jt += 32, buf ^= 1) {
+            __syncthreads();                               // tile jt visible; tile jt-32's buffer free
+            if (jt + 32 < j1) {
+                lstore(buf ^ 1);                           // tile jt+32 (loaded one iteration ago)
+#if !(defined(VO_MATCH_DIAG) && VO_MATCH_DIAG == 2)
+                if (jt + 64 < j1) gload(jt + 64);          // (diagnostic build 2: no F2 loads after the first)
+#endif
+            }
+            v4i b[4];
+            const uint8_t* brow = &bt[buf][l31 * MP_LDS_ROW + 16 * h];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) b[kk] = *reinterpret_cast<const v4i*>(brow + 32 * kk);
+            const int ck = bck[buf][l31];
+            const float inb = binb[buf][l31];
+            v16i accv = (v16i){0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) accv = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kk], b[kk], accv, 0, 0, 0);
+            const int jc = jt + l31;
+            // ragged last tile: masked columns get c = -inf (never ranked); elsewhere c + 0 = c
+            // exactly (c >= +0)
+            const float cmask = jc < j1 ? 0.0f : -INFINITY;
+#if defined(VO_MATCH_DIAG) && VO_MATCH_DIAG == 1
+            // diagnostic build 1 (timing only): no epilogue, the accumulators feed one running max
+            for (int reg = 0; reg < 16; ++reg) best[reg] = fmaxf(best[reg], (float)accv[reg] + cmask);
+#else
+#pragma unroll
+            for (int reg = 0; reg < 16; reg += 2) {
+                // c for two accumulator rows at once: the two products as packed f32 muls
+                // (each component an IEEE multiply, same bits as the scalar form)
+                const vo_f2 fp = vo_f2{(float)(accv[reg] + rk[reg] + ck), (float)(accv[reg + 1] + rk[reg + 1] + ck)};
+                vo_f2 cp = (fp * vo_f2{ina[reg], ina[reg + 1]}) * vo_f2{inb, inb};
+                cp = cp + vo_f2{cmask, cmask};
+#pragma unroll
+                for (int h2 = 0; h2 < 2; ++h2) {
+                    const int q = reg + h2;
+                    const float c = h2 ? cp.y : cp.x;
+                    if (__builtin_amdgcn_ballot_w64(c > second[q])) {
+                        const bool g1 = c > best[q], g2 = c > second[q];
+                        second[q] = g1 ? best[q] : (g2 ? c : second[q]);
+                        best[q] = g1 ? c : best[q];
+                        bidx[q] = g1 ? jc : bidx[q];
+                    }
+                }
+            }
+#endif
+            ++tno;
+            if ((tno & (tno - 1)) == 0) {                  // wave-uniform
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg) second[reg] = half_max(second[reg]);
+            }
+        }
+        // merge the 32 lanes of each half (same accumulator rows, different columns)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) half_top2c(best[reg], bidx[reg], second[reg]);
         if (l31 < 16) {
-            float bb, ss;
-            int ii;
-            mp_row_result(l31, best, bidx, second, bb, ii, ss);
-            const int row = mp_lane_row(blk * MP_ROWS + 32 * wave, l31, h);
+            // lane l31 of half h writes accumulator row `l31` (select by unrolled compare)
+            float bb = -INFINITY, ss = -INFINITY;
+            int ii = -1;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg)
+                if (reg == l31) { bb = best[reg]; ii = bidx[reg]; ss = second[reg]; }
+            const int row = i0 + (l31 & 3) + 8 * (l31 >> 2) + 4 * h;
             if (row < n1) {
                 MatchTop2 m;
                 m.best = bb; m.idx = ii; m.second = ss; m.pad = 0;
@@ -417,131 +381,6 @@ __global__ __launch_bounds__(1024) void k_match_compact(const MatchJob* __restri
         }
     }
     if (tid == 0) gst(J.out_n, (int)(total < (uint32_t)J.cap ? total : (uint32_t)J.cap));
-}
-
-__device__ __forceinline__ uint32_t block_exscan_256(uint32_t v, uint32_t* sh, uint32_t* total)
-{
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) sh[wid] = x;
-    __syncthreads();
-    uint32_t before = 0;
-    for (int w = 0; w < wid; ++w) before += sh[w];
-    *total = sh[0] + sh[1] + sh[2] + sh[3];
-    __syncthreads();
-    return before + x - v;
-}
-
-// One step s of find_remaining_points (VO.m:283-333: lm, rm, cm, last) for every frame of the
-// batch: grid (W, B), workgroup (x, f) takes F1 row blocks x, x + W, ... of frame f's step-s
-// match and
-//   (1) matches them against all F2 columns (mp_block over the whole column range as one
-//       chunk: the same exact top-2 that k_match_partial + k_match_merge reach over chunks,
-//       since the merge is an order-free (value, index) rule) and applies MatchThreshold and
-//       MaxRatio in place (k_match_merge's test) -> res[row];
-// the frame's last workgroup to finish (a per-frame counter; no workgroup ever waits) then
-//   (2) compacts the accepted rows in ascending F1 order (k_match_compact's rule) and
-//   (3) composes the index lists (k_compose; VO.m:287-290 / 297-308 / 314-317 / 326-333).
-// So each step is one launch instead of four (partial, merge, compact, compose), and the next
-// step's row counts are the list lengths this one leaves.
-__global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_track_step(TrackArgs a, int s)
-{
-    __shared__ __attribute__((aligned(16))) MpTiles T;
-    __shared__ uint32_t wsum[4];
-    __shared__ int s_last;
-    const int x = blockIdx.x, W = gridDim.x, f = blockIdx.y;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l31 = lane & 31;
-    const int K = a.kp_cap, M = a.M;
-    int* res = a.res + (size_t)f * a.row_cap;
-    const MatchJob J = a.jobs[s * M + f];
-    const int n1 = job_rows(J.n1, a.row_cap), n2 = job_rows(J.n2, a.row_cap);
-    if (n2 == 0) {
-        for (int r = x * 256 + tid; r < n1; r += W * 256) res[r] = -1;
-    } else {
-        for (int i0b = x * MP_ROWS; i0b < n1; i0b += W * MP_ROWS) {      // workgroup-uniform
-            float best[16], second[16];
-            int bidx[16];
-            mp_block(J, n1, i0b, 0, n2, T, best, bidx, second);
-            if (l31 < 16) {
-                float bb, ss;
-                int ii;
-                mp_row_result(l31, best, bidx, second, bb, ii, ss);
-                const int row = mp_lane_row(i0b + 32 * wave, l31, h);
-                if (row < n1) {
-                    float b = -INFINITY, sv = -INFINITY;
-                    int i = -1;
-                    top2c_merge(b, i, sv, bb, ii, ss);          // k_match_merge over one chunk
-                    const float bs = 2.0f - 2.0f * b, ssd2 = 2.0f - 2.0f * sv;
-                    res[row] = (i >= 0 && bs <= a.T && (bs / ssd2) <= a.max_ratio) ? i : -1;
-                }
-            }
-        }
-    }
-    // release this workgroup's rows (device scope: the other workgroups may sit on other XCDs);
-    // the W-th arrival goes on, with an acquire before it reads any row
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) s_last = atomicAdd(a.cnt + f, 1) == W - 1;
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    // accepted rows in ascending F1 order
-    const int chunk = (n1 + 255) / 256;
-    const int r0 = min(tid * chunk, n1), r1 = min(r0 + chunk, n1);
-    uint32_t cnt = 0;
-    for (int r = r0; r < r1; ++r) cnt += __hip_atomic_load(res + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 0;
-    uint32_t total;
-    uint32_t base = block_exscan_256(cnt, wsum, &total);
-    for (int r = r0; r < r1; ++r) {
-        const int i = __hip_atomic_load(res + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (i >= 0) {
-            if (base < (uint32_t)J.cap) { gst(J.out_i + base, r); gst(J.out_j + base, i); }
-            base++;
-        }
-    }
-    const int n_out = (int)(total < (uint32_t)J.cap ? total : (uint32_t)J.cap);
-    if (tid == 0) { gst(J.out_n, n_out); a.cnt[f] = 0; }      // the counter is ready for the next step
-    __syncthreads();
-    // index composition (k_compose)
-    int* L = a.lists + (size_t)f * TL_COUNT * K;
-    const int pp = f ? f - 1 : M;
-    const int n = min(n_out, K);
-    for (int k = tid; k < n; k += 256) {
-        const int i = gld(J.out_i + k), j = gld(J.out_j + k);
-        if (s == 0) {
-            L[TL_OL1 * K + k] = a.pair_i[(size_t)pp * K + j];
-            L[TL_OR1 * K + k] = a.pair_j[(size_t)pp * K + j];
-            L[TL_CL * K + k] = i;
-        } else if (s == 1) {
-            L[TL_OL2 * K + k] = L[TL_OL1 * K + j];
-            L[TL_OR2 * K + k] = L[TL_OR1 * K + j];
-            L[TL_CR * K + k] = i;
-        } else if (s == 2) {
-            L[TL_CL2 * K + k] = L[TL_CL * K + i];
-            L[TL_CR2 * K + k] = L[TL_CR * K + j];
-        } else {
-            L[TL_OLF * K + k] = L[TL_OL2 * K + j];
-            L[TL_ORF * K + k] = L[TL_OR2 * K + j];
-            L[TL_CLF * K + k] = L[TL_CL2 * K + i];
-            L[TL_CRF * K + k] = L[TL_CR2 * K + i];
-        }
-    }
-    if (tid == 0) a.list_n[4 * f + s] = n;
-}
-
-#ifndef VO_TRACK_W
-#define VO_TRACK_W 8              // workgroups per frame and step (row blocks of 128 F1 rows each)
-#endif
-void track_fused_launch(const TrackArgs& a, int B, hipStream_t s)
-{
-    if (B <= 0) return;
-    for (int step = 0; step < 4; ++step)
-        VO_LAUNCH(k_track_step, dim3(VO_TRACK_W, B), dim3(256), 0, s, a, step);
 }
 
 // Descriptor metadata for externally supplied descriptors (vo_match on host data).

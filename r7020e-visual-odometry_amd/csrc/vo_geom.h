@@ -42,7 +42,6 @@ struct GeomBuffers {
     uint8_t* inliers = nullptr;  // [max_frames][kp_cap]
     MsacHyp* hyp = nullptr;      // [max_frames][n_hyp]
     FrameGeom* fg = nullptr;     // [max_frames]
-    int* track_cnt = nullptr;    // [max_frames] k_track_step arrival counters (zero between launches)
     // landmarks
     float* spos = nullptr;       // [max_frames][kp_cap][4] stereo subset positions (lx, ly, rx, ry)
     int* s_n = nullptr;          // [max_frames]
@@ -79,21 +78,6 @@ struct StepArgs {
 // landmark kernels for frames [0, B).  match jobs at d_jobs + first.
 void geom_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_track_jobs, const StepArgs& a,
                   const vo_match_params& mp, hipStream_t s);
-// find_remaining_points (VO.m:283-333) as four launches, one per dependent match: each runs
-// the match of every frame, its compaction in ascending F1 order and its index composition
-// (csrc/match.hip k_track_step).  jobs: the track jobs (step s of frame f at jobs[s * M + f]);
-// res: per-frame scratch rows [B][row_cap]; cnt: per-frame arrival counters [B], zero between
-// launches.
-struct TrackArgs {
-    const MatchJob* jobs;
-    int M, kp_cap, row_cap;
-    int* lists; int* list_n;
-    const int* pair_i; const int* pair_j;     // stereo pairs per pair slot (frame f-1's, or slot M)
-    int* res;
-    int* cnt;
-    float T, max_ratio;
-};
-void track_fused_launch(const TrackArgs& a, int B, hipStream_t s);
 // tracking only (4 matches + compositions); lists/list_n valid afterwards.
 void track_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_track_jobs, const StepArgs& a,
                    const vo_match_params& mp, hipStream_t s);
