@@ -943,6 +943,16 @@ void track_enqueue(GeomBuffers& g, const MatchBuffers& mb, const MatchJob* d_tra
                    const vo_match_params& mp, hipStream_t s)
 {
     const int B = a.B, M = a.max_frames, K = a.kp_cap;
+#ifndef VO_MATCH_FINISH
+#define VO_MATCH_FINISH 1         // the composition inside match_launch's finishing kernel (csrc/match.hip)
+#endif
+    if (VO_MATCH_FINISH) {
+        for (int step = 0; step < 4; ++step) {
+            MatchCompose cp{g.lists, g.list_n, a.pair_i, a.pair_j, M, K, step, 0};
+            match_launch(mb, d_track_jobs + step * M, B, mp, s, &cp);
+        }
+        return;
+    }
     ComposeArgs ca;
     ca.lists = g.lists; ca.list_n = g.list_n; ca.step_i = g.step_i; ca.step_j = g.step_j; ca.step_n = g.step_n;
     ca.pair_i = a.pair_i; ca.pair_j = a.pair_j; ca.pair_n = a.pair_n; ca.M = M; ca.kp_cap = K;

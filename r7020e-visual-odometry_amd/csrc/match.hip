@@ -14,6 +14,7 @@
 // MaxRatio; k_match_compact writes the pairs in ascending F1 order with a block
 // prefix sum.
 #include "vo_internal.h"
+#include "vo_geom.h"
 
 namespace vo {
 
@@ -383,6 +384,80 @@ __global__ __launch_bounds__(1024) void k_match_compact(const MatchJob* __restri
     if (tid == 0) gst(J.out_n, (int)(total < (uint32_t)J.cap ? total : (uint32_t)J.cap));
 }
 
+// One 256-thread workgroup per job: k_match_merge + k_match_compact (+ k_compose) in one
+// launch.  Rows go in tiles of 256 in ascending F1 order (coalesced partial reads): thread t
+// merges row 256 k + t over the F2 chunks and applies MatchThreshold / MaxRatio; the tile's
+// accepted rows are placed by a block prefix sum after the running count, so the pairs come
+// out in ascending F1 order exactly as k_match_compact writes them.  With `compose` (a
+// tracking step of find_remaining_points), the workgroup then applies that step's index
+// composition to its frame's lists (k_compose, VO.m:287-333) -- so a tracking step is two
+// launches (partial, finish) instead of four.
+__global__ __launch_bounds__(256) void k_match_finish(const MatchJob* __restrict__ jobs, const MatchTop2* __restrict__ partial,
+                                                      int row_cap, int n_chunks_cap, float T, float max_ratio,
+                                                      MatchCompose cp, int with_compose)
+{
+    __shared__ uint32_t wsum[4];
+    const int jb = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const MatchJob J = jobs[jb];
+    const int n1 = job_rows(J.n1, row_cap), n2 = job_rows(J.n2, row_cap);
+    const int nch = (n2 + VO_MATCH_CHUNK - 1) / VO_MATCH_CHUNK;
+    const MatchTop2* P = partial + (size_t)jb * n_chunks_cap * row_cap;
+    uint32_t base = 0;
+    for (int r0 = 0; r0 < n1; r0 += 256) {                       // block-uniform
+        const int r = r0 + tid;
+        int acc = -1;
+        if (r < n1) {
+            float b = -INFINITY, s = -INFINITY;
+            int i = -1;
+            for (int c = 0; c < nch; ++c) {
+                const MatchTop2 m = P[(size_t)c * row_cap + r];
+                top2c_merge(b, i, s, m.best, m.idx, m.second);
+            }
+            const float bs = 2.0f - 2.0f * b, ss = 2.0f - 2.0f * s;      // SSD of best / second best
+            acc = (i >= 0 && bs <= T && (bs / ss) <= max_ratio) ? i : -1;
+        }
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(acc >= 0);
+        if (lane == 0) wsum[wid] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t before = base;
+        for (int w = 0; w < wid; ++w) before += wsum[w];
+        const uint32_t pos = before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+        if (acc >= 0 && pos < (uint32_t)J.cap) { gst(J.out_i + pos, r); gst(J.out_j + pos, acc); }
+        base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();                                          // wsum reused by the next tile
+    }
+    const int n_out = (int)(base < (uint32_t)J.cap ? base : (uint32_t)J.cap);
+    if (tid == 0) gst(J.out_n, n_out);
+    if (!with_compose) return;
+    __syncthreads();                                              // the pairs are visible to the block
+    // k_compose of tracking step cp.step for frame f = jb
+    const int f = cp.f0 + jb, K = cp.kp_cap, M = cp.M, st = cp.step;
+    int* L = cp.lists + (size_t)f * TL_COUNT * K;
+    const int pp = f ? f - 1 : M;
+    const int n = min(n_out, K);
+    for (int k = tid; k < n; k += 256) {
+        const int i = gld(J.out_i + k), j = gld(J.out_j + k);
+        if (st == 0) {
+            L[TL_OL1 * K + k] = cp.pair_i[(size_t)pp * K + j];
+            L[TL_OR1 * K + k] = cp.pair_j[(size_t)pp * K + j];
+            L[TL_CL * K + k] = i;
+        } else if (st == 1) {
+            L[TL_OL2 * K + k] = L[TL_OL1 * K + j];
+            L[TL_OR2 * K + k] = L[TL_OR1 * K + j];
+            L[TL_CR * K + k] = i;
+        } else if (st == 2) {
+            L[TL_CL2 * K + k] = L[TL_CL * K + i];
+            L[TL_CR2 * K + k] = L[TL_CR * K + j];
+        } else {
+            L[TL_OLF * K + k] = L[TL_OL2 * K + j];
+            L[TL_ORF * K + k] = L[TL_OR2 * K + j];
+            L[TL_CLF * K + k] = L[TL_CL2 * K + i];
+            L[TL_CRF * K + k] = L[TL_CR2 * K + i];
+        }
+    }
+    if (tid == 0) cp.list_n[4 * f + st] = n;
+}
+
 // Descriptor metadata for externally supplied descriptors (vo_match on host data).
 __global__ void k_desc_meta(const uint8_t* __restrict__ desc, DescMeta* __restrict__ meta, int n)
 {
@@ -426,18 +501,40 @@ MatchBuffers match_view(const MatchBuffers& b, int k0)
     return v;
 }
 
-void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, const vo_match_params& p, hipStream_t s)
+#ifndef VO_MATCH_FINISH
+#define VO_MATCH_FINISH 1         // 0: k_match_merge + k_match_compact (+ k_compose) as separate launches
+#endif
+void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, const vo_match_params& p, hipStream_t s,
+                  const MatchCompose* compose)
 {
     if (n_jobs <= 0) return;
     if (n_jobs > VO_MP_MAX_JOBS) {                       // the task table holds VO_MP_MAX_JOBS jobs
-        match_launch(b, d_jobs, VO_MP_MAX_JOBS, p, s);
-        match_launch(match_view(b, VO_MP_MAX_JOBS), d_jobs + VO_MP_MAX_JOBS, n_jobs - VO_MP_MAX_JOBS, p, s);
+        MatchCompose rest;
+        if (compose) {                                   // frames VO_MP_MAX_JOBS.. of a tracking step
+            rest = *compose;
+            rest.f0 += VO_MP_MAX_JOBS;
+        }
+        match_launch(b, d_jobs, VO_MP_MAX_JOBS, p, s, compose);
+        match_launch(match_view(b, VO_MP_MAX_JOBS), d_jobs + VO_MP_MAX_JOBS, n_jobs - VO_MP_MAX_JOBS, p, s,
+                     compose ? &rest : nullptr);
         return;
     }
     VO_LAUNCH(k_match_partial, dim3(2048), dim3(256), 0, s, d_jobs, n_jobs, b.partial, b.row_cap, b.n_chunks);
+    if (VO_MATCH_FINISH) {
+        MatchCompose cp{};
+        if (compose) cp = *compose;
+        VO_LAUNCH(k_match_finish, dim3(n_jobs), dim3(256), 0, s, d_jobs, (const MatchTop2*)b.partial, b.row_cap, b.n_chunks,
+                  p.match_threshold * 0.04f, p.max_ratio, cp, compose ? 1 : 0);
+        return;
+    }
     VO_LAUNCH(k_match_merge, dim3((b.row_cap + 255) / 256, n_jobs), dim3(256), 0, s, d_jobs, (const MatchTop2*)b.partial,
               b.res, b.row_cap, b.n_chunks, p.match_threshold * 0.04f, p.max_ratio);
     VO_LAUNCH(k_match_compact, dim3(n_jobs), dim3(1024), 0, s, d_jobs, (const int*)b.res, b.row_cap);
+}
+
+void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, const vo_match_params& p, hipStream_t s)
+{
+    match_launch(b, d_jobs, n_jobs, p, s, nullptr);
 }
 
 // single-precision descriptor matrix (MATLAB's extractFeatures output: n x 128 single, integer

@@ -258,6 +258,17 @@ MatchBuffers match_view(const MatchBuffers& b, int k0);
 void match_free(MatchBuffers& b);
 // d_jobs: device array of n_jobs jobs (prepared once per context); job k uses
 // partial-result slot k.
+// The index composition after tracking step `step` of find_remaining_points (VO.m:287-290,
+// 297-300, 305-308, 314-317, 326-333) over lists [frame][TL_COUNT][kp_cap] (vo_geom.h), applied
+// by match_launch's finishing kernel to the step's compacted pairs of job f (= frame f).
+struct MatchCompose {
+    int* lists; int* list_n;
+    const int* pair_i; const int* pair_j;    // stereo pairs per pair slot (frame f-1's, or slot M)
+    int M, kp_cap, step;
+    int f0;                                  // frame of job 0 (a launch split at VO_MP_MAX_JOBS jobs)
+};
+void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, const vo_match_params& p,
+                  hipStream_t s, const MatchCompose* compose);
 void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, const vo_match_params& p,
                   hipStream_t s);
 void desc_meta_launch(const uint8_t* desc, DescMeta* meta, int n, hipStream_t s);

@@ -252,26 +252,28 @@ def test_sequence_kitti_resolution_bit_exact(vo, oracle, syn):
     ctx.close()
 
 
-def test_full_path_batch_128_equals_two_batches_of_64(vo, syn, calib):
-    """The whole loop body at the largest batch (128 chained frames in one vo_step_batch_dev
-    call: 258 image slots, 641 match jobs split over three match launches) gives the same
-    per-frame outputs and landmark map as the same frames in two 64-frame calls (that path is
-    pinned to the oracle by the tests above)."""
+@pytest.mark.parametrize("B", [128, 320])
+def test_full_path_big_batch_equals_batches_of_64(vo, syn, calib, B):
+    """The whole loop body at a large batch (B chained frames in one vo_step_batch_dev call: at
+    320, over 256 match jobs per launch, so the stereo and tracking launches split at
+    VO_MP_MAX_JOBS and the second part's frames compose their lists at frame offset 256) gives
+    the same per-frame outputs and landmark map as the same frames in 64-frame calls (that path
+    is pinned to the oracle by the tests above)."""
     import torch
     SL, SR, _ = syn.sequence(32, 375, 1242, seed=syn.SEED_BASE + 0x777, step_m=0.25, yaw_deg=0.1)
-    loop = np.arange(128) % 64
+    loop = np.arange(B) % 64
     loop = np.where(loop < 32, loop, 63 - loop)
     L, R = np.ascontiguousarray(SL[loop]), np.ascontiguousarray(SR[loop])
     dl, dr = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
     torch.cuda.synchronize()
     fs = L[0].size
-    big = vo.Context(375, 1242, 128, calib=calib)
-    a = big.step_batch_dev(dl.data_ptr(), dr.data_ptr(), 128)
+    big = vo.Context(375, 1242, B, calib=calib)
+    a = big.step_batch_dev(dl.data_ptr(), dr.data_ptr(), B)
     lm_a = big.get_landmarks()
     big.close()
     half = vo.Context(375, 1242, 64, calib=calib)
-    b = np.concatenate([half.step_batch_dev(dl.data_ptr(), dr.data_ptr(), 64),
-                        half.step_batch_dev(dl.data_ptr() + 64 * fs, dr.data_ptr() + 64 * fs, 64)])
+    b = np.concatenate([half.step_batch_dev(dl.data_ptr() + b0 * fs, dr.data_ptr() + b0 * fs, 64)
+                        for b0 in range(0, B, 64)])
     lm_b = half.get_landmarks()
     half.close()
     assert (a["status"][1:] == 0).all()
