@@ -99,6 +99,33 @@ def launch_ranks(n: int) -> int:
     return p.wait()
 
 
+def feature_traffic(fmodel, kt, kt_iso, profile_steps, B):
+    """Per-kernel feature-stage bytes of one call: the algorithmic and line-floor model
+    (roofline.feature_bytes) beside the PMC traffic of the same workload (TRAFFIC_FILE: FETCH_SIZE
+    x 2 + WRITE_SIZE, per launch x launches per call) and the algorithmic GB/s in situ / isolated."""
+    tr = json.loads(TRAFFIC_FILE.read_text())["kernels"] if TRAFFIC_FILE.exists() else {}
+    calls = tr.get("k_blur_base", {}).get("launches", 0) or 1       # one octave-0 base launch per call
+    out, tot_pmc, tot_alg = {}, 0.0, 0.0
+    for name, m in fmodel.items():
+        e = {"algorithmic_bytes": m["algorithmic"], "line_floor_bytes": m["line_floor"]}
+        t = tr.get(name)
+        if t:
+            pmc = t["hbm_bytes_per_launch"] * t["launches"] / calls
+            e.update(pmc_bytes=pmc, pmc_over_algorithmic=pmc / m["algorithmic"] if m["algorithmic"] else None,
+                     pmc_over_line_floor=pmc / m["line_floor"] if m["line_floor"] else None)
+            tot_pmc += pmc
+        tot_alg += m["algorithmic"]
+        if name in kt and kt[name][0] > 0:
+            e["gbs_in_situ"] = round(m["algorithmic"] / (kt[name][0] / profile_steps * 1e-3) / 1e9, 1)
+        if name in kt_iso and kt_iso[name][0] > 0:
+            e["gbs_isolated"] = round(m["algorithmic"] / (kt_iso[name][0] / profile_steps * 1e-3) / 1e9, 1)
+        out[name] = e
+    return {"kernels": out, "pmc_gb_per_64_frames": tot_pmc / 1e9 * 64 / B, "algorithmic_gb_per_64_frames": tot_alg / 1e9 * 64 / B,
+            "traffic_source": str(TRAFFIC_FILE.relative_to(ROOT)) if TRAFFIC_FILE.exists() else None,
+            "note": "per call of --batch frames; PMC of the kernels the traffic file holds (FETCH_SIZE calibrated at 1/2 of "
+                    "the 128-B line bytes for these access shapes, profiles/r06_c_fetch_calib.txt)"}
+
+
 def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks, gather_over_ranks):
     """KITTI-00 (BASELINE configs[2] at N=1, configs[3] at N=8): frames rendered along the
     reference's ground truth (street.py) into HBM -- each rank only its block + halo -- then
@@ -410,6 +437,17 @@ def main():
     roof["kernel_ms_per_step"] = {n: round(v[0] / args.profile_steps, 4) for n, v in sorted(kt.items(), key=lambda kv: -kv[1][0])}
     roof["kernel_ms_per_step_isolated"] = {n: round(v[0] / args.profile_steps, 4)
                                            for n, v in sorted(kt_iso.items(), key=lambda kv: -kv[1][0])}
+
+    # ---- feature stages: byte model from this call's counts against the PMC traffic ----
+    # (the last call's results: the same frames as every call of the loop)
+    nc = np.array([ctx.fetch_candidate_counts(i) for i in range(2 * B)])
+    kps = [ctx.fetch_keypoints(i, descriptors=False)[0] for i in range(2 * B)]
+    allk = np.concatenate(kps)
+    fmodel = roofline.feature_bytes(ROWS, COLS, nc[:, 0], nc[:, 1], allk["size"], allk["octave"], allk["angle"],
+                                    np.repeat(np.arange(2 * B), [len(k) for k in kps]), [s_[:3] for s_ in stats])
+    roof["feature_traffic"] = feature_traffic(fmodel, kt, kt_iso, args.profile_steps, B)
+    roof["feature_traffic"]["mean_candidates_per_image"] = float(nc[:, 0].mean())
+    roof["feature_traffic"]["mean_accepted_per_image"] = float(nc[:, 1].mean())
 
     # ---- BASELINE configs[2]/[3]: the full per-frame path over the KITTI-00 trajectory ----
     full = None

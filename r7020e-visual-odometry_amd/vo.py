@@ -334,15 +334,17 @@ class Context:
             return [(s.n_left, s.n_right, s.n_stereo, s.flags) for s in st]
         return None
 
-    def fetch_keypoints(self, image: int):
+    def fetch_keypoints(self, image: int, descriptors: bool = True):
+        """(keypoints, descriptors) of `image` in the last batched call; descriptors=False
+        skips the descriptor copy (returns None for them)."""
         cap = self.sift_params.max_keypoints
         kps = np.zeros(cap, KP_DTYPE)
-        desc = np.zeros((cap, 128), np.uint8)
+        desc = np.zeros((cap, 128), np.uint8) if descriptors else None
         n = C.c_int(0)
         self._check(self.lib.vo_fetch_keypoints(self.h, image, kps.ctypes.data_as(C.POINTER(Keypoint)),
-                                                _p(desc, C.c_uint8), cap, C.byref(n)))
+                                                _p(desc, C.c_uint8) if descriptors else None, cap, C.byref(n)))
         m = min(n.value, cap)
-        return kps[:m].copy(), desc[:m].copy()
+        return kps[:m].copy(), (desc[:m].copy() if descriptors else None)
 
     def fetch_candidate_counts(self, image: int) -> tuple[int, int]:
         """(extremum candidates, candidates accepted by the refinement) of `image` in the last
