@@ -177,6 +177,21 @@ def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks,
     el = max_over_ranks(el)
     t_tail = max_over_ranks(t_tail)
     n_lm = int(np.asarray(steps["n_landmarks"]).sum())
+    # load balance of the block partition: measured over this run's ranks, and projected for
+    # 2 / 4 / 8 ranks from this run's per-frame keypoint counts (the SIFT + descriptor work, the
+    # bulk of a frame's cost, scales with them; the scale space is the same for every frame)
+    kp_cost = np.asarray(steps["n_left"], np.float64) + np.asarray(steps["n_right"], np.float64)
+    loops = [v[0] for v in per_rank]
+    proj = {str(w): round(sharding.block_imbalance(kp_cost, w), 4) for w in (2, 4, 8)}
+    # projected 8-rank efficiency: each rank's loop = this run's per-frame loop time x its block
+    # (1/8 of the frames + a halo frame) x the block's cost imbalance, plus a ~3 ms tail
+    t1 = el * world / max(n, 1)                     # s per frame on one rank
+    t8 = t1 * (n / 8 + 1) * proj["8"] + 3e-3
+    balance = {"loop_max_over_mean": round(max(loops) / (sum(loops) / len(loops)), 4) if world > 1 else None,
+               "projected_block_cost_max_over_mean": proj,
+               "cost_proxy": "keypoints per frame (n_left + n_right), halo frame included",
+               "projected_8_rank_efficiency": round((n * t1) / (8 * t8), 4) if world == 1 else None,
+               "projected_8_rank_note": "N=1 per-frame time x (1/8 of the frames + halo) x block cost imbalance + 3 ms tail"}
     if lm is not None and len(lm) != n_lm:
         raise RuntimeError(f"landmark map has {len(lm)} rows, the records {n_lm}")
     # per-kernel HIP-event durations of the full path over the block's first PB batches (a
@@ -221,6 +236,7 @@ def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks,
             "mean_stereo_matches": float(steps["n_stereo"].mean()), "mean_tracked": float(steps["n_tracked"][1:].mean()),
             "landmark_rows": n_lm,
             "tail_ms": round(t_tail * 1e3, 3),
+            "load_balance": balance,
             "per_rank_ms": [{"rank": r, "loop": round(v[0] * 1e3, 2), "tail": round(v[1] * 1e3, 3),
                              "records": round(v[2] * 1e3, 3), "chain": round(v[3] * 1e3, 3),
                              "world": round(v[4] * 1e3, 3), "map": round(v[5] * 1e3, 3)}

@@ -36,6 +36,19 @@ def shard_range(n_frames: int, world: int, rank: int) -> tuple[int, int]:
     return start, start + base + (1 if rank < rem else 0)
 
 
+def block_imbalance(cost, world: int) -> float:
+    """max / mean over ranks of the per-block cost of `shard_range`'s partition (each rank > 0
+    also recomputes its halo frame), for a per-frame cost proxy such as the keypoint count."""
+    cost = np.asarray(cost, np.float64)
+    n = len(cost)
+    tot = []
+    for r in range(world):
+        s, e = shard_range(n, world, r)
+        tot.append(cost[halo_start(s):e].sum() if e > s else 0.0)
+    tot = np.asarray(tot)
+    return float(tot.max() / tot.mean()) if tot.mean() > 0 else 1.0
+
+
 def halo_start(start: int) -> int:
     """First frame a rank must process: one frame before its block (halo)."""
     return start - 1 if start > 0 else 0

@@ -76,3 +76,29 @@ def test_libvo_host_chain_and_landmark_transform_equal_references(vo, oracle):
     assert np.all(got[~keep] == 0)
     with pytest.raises(vo.VOError):
         vo.landmarks_to_world_frames(poses, n + 1, X, keep)
+
+
+def test_block_imbalance():
+    """sharding.block_imbalance: max / mean of the partition's per-block cost (halo included)."""
+    from r7020e_visual_odometry_amd import sharding
+    assert sharding.block_imbalance(np.ones(8), 1) == 1.0
+    # 8 frames over 2 ranks: rank 0 frames 0-3 (4), rank 1 halo 3 + frames 4-7 (5): 5 / 4.5
+    assert abs(sharding.block_imbalance(np.ones(8), 2) - 5 / 4.5) < 1e-12
+    cost = np.r_[np.full(4, 10.0), np.ones(4)]                       # heavy first half
+    assert abs(sharding.block_imbalance(cost, 2) - 40 / ((40 + 14) / 2)) < 1e-12
+
+
+def test_feature_byte_model():
+    """roofline.feature_bytes: mask geometry of the extremum test and window pricing."""
+    from r7020e_visual_odometry_amd import roofline
+    w, s = roofline.mask_geometry(375, 1242)
+    # octave 0 (750 x 2484): 740 interior rows x 40 words x 3 layers, dominant
+    assert w > 3 * 740 * 38 and s == (w + 1023) // 1024
+    one = roofline.feature_bytes(375, 1242, [100], [50], [5.0], [0], [0.0], [0], [(10, 10, 5)])
+    two = roofline.feature_bytes(375, 1242, [200], [100], [5.0, 5.0], [0, 0], [0.0, 0.0], [0, 0], [(10, 10, 5)])
+    assert two["k_refine"]["algorithmic"] > one["k_refine"]["algorithmic"]
+    for k, v in one.items():
+        assert v["line_floor"] >= v["algorithmic"] > 0, k
+    # a larger keypoint reads a larger descriptor window
+    big = roofline.feature_bytes(375, 1242, [100], [50], [20.0], [0], [0.0], [0], [(10, 10, 5)])
+    assert big["k_desc"]["algorithmic"] > one["k_desc"]["algorithmic"]
