@@ -70,7 +70,9 @@ def parse():
     ap.add_argument("--concurrency", type=int, default=0, help="forked streams per batch (0: library default)")
     ap.add_argument("--seq-frames", type=int, default=4541,
                     help="KITTI-00 trajectory frames through the full per-frame path, sharded over the ranks (0: skip)")
-    ap.add_argument("--seq-batch", type=int, default=64, help="frames per vo_step_submit_dev call in the sequence leg")
+    ap.add_argument("--seq-batch", type=int, default=256,
+                    help="frames per vo_step_submit_dev call in the sequence leg (3 in flight; 64: 8644, 128: 8862, "
+                         "256: 9128 stereo frames/s, profiles/r06_b_seq_*)")
     ap.add_argument("--dry-run", action="store_true",
                     help="rendezvous only (gloo, no GPU): rank 0 prints the world size it sees (launcher test)")
     ap.add_argument("--large-batch", type=int, default=128,
@@ -464,6 +466,8 @@ def main():
     roof["feature_traffic"] = feature_traffic(fmodel, kt, kt_iso, args.profile_steps, B)
     roof["feature_traffic"]["mean_candidates_per_image"] = float(nc[:, 0].mean())
     roof["feature_traffic"]["mean_accepted_per_image"] = float(nc[:, 1].mean())
+    ctx.close()                                                # the legs below make their own contexts
+    del d_l, d_r
 
     # ---- BASELINE configs[2]/[3]: the full per-frame path over the KITTI-00 trajectory ----
     full = None
