@@ -279,3 +279,34 @@ def test_full_path_big_batch_equals_batches_of_64(vo, syn, calib, B):
     assert (a["status"][1:] == 0).all()
     assert a.tobytes() == b.tobytes()
     assert lm_a.shape == lm_b.shape and lm_a.tobytes() == lm_b.tobytes()
+
+
+def test_full_path_bench_configuration_pipelined(vo, syn, calib):
+    """bench.py's full-path configuration: 256 frames per vo_step_submit_dev, three batches in
+    flight (kitti._pipelined's default depth), camera-frame landmark rows kept on the device --
+    equal, frame for frame and row for row, to the same 768 chained frames in 64-frame
+    synchronous calls (pinned to the oracle by the tests above)."""
+    import torch
+    from r7020e_visual_odometry_amd import kitti
+    SL, SR, _ = syn.sequence(32, 375, 1242, seed=syn.SEED_BASE + 0x778, step_m=0.25, yaw_deg=0.1)
+    n = 768
+    loop = np.arange(n) % 64
+    loop = np.where(loop < 32, loop, 63 - loop)
+    L, R = np.ascontiguousarray(SL[loop]), np.ascontiguousarray(SR[loop])
+    dl, dr = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+    torch.cuda.synchronize()
+    fs = L[0].size
+    big = vo.Context(375, 1242, 256, calib=calib)
+    big.set_landmark_frame(True)
+    a = np.concatenate(kitti._pipelined(big, kitti.device_batches(dl, dr, 256), torch.device("cuda", 0)))
+    Xa, ka = big.get_landmark_rows()
+    big.close()
+    half = vo.Context(375, 1242, 64, calib=calib)
+    half.set_landmark_frame(True)
+    b = np.concatenate([half.step_batch_dev(dl.data_ptr() + b0 * fs, dr.data_ptr() + b0 * fs, 64)
+                        for b0 in range(0, n, 64)])
+    Xb, kb = half.get_landmark_rows()
+    half.close()
+    assert (a["status"][1:] == 0).all() and len(a) == n
+    assert a.tobytes() == b.tobytes()
+    assert Xa.tobytes() == Xb.tobytes() and ka.tobytes() == kb.tobytes()
