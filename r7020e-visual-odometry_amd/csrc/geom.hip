@@ -869,25 +869,29 @@ __global__ __launch_bounds__(1024) void k_lm_filter(const float* __restrict__ sp
     }
 }
 
-// CreateLandmarksFromFeatures: odd 1-based rows (even 0-based), triangulate, z gates.
+// CreateLandmarksFromFeatures: odd 1-based rows (even 0-based), triangulate, z gates.  Every
+// row up to max(M, 2) is written: the kept point, or a zero row (odd rows, rows failing a z
+// gate, and the two preallocated rows of CreateLandmarksFromFeatures.m:2 when M < 2) -- the
+// camera-frame rows vo_get_landmark_rows returns equal oracle_landmark_rows', zero rows included.
 __global__ void k_lm_tri(const float* __restrict__ spos, const int* __restrict__ lm_new, const int* __restrict__ lm_M,
                          int kp_cap, CalibDev cal, float* __restrict__ lm_X, uint8_t* __restrict__ lm_keep,
                          int* __restrict__ lm_rows)
 {
     const int f = blockIdx.y, K = kp_cap;
     const int M = lm_M[f];
-    for (int m = blockIdx.x * blockDim.x + threadIdx.x; m < M; m += gridDim.x * blockDim.x) {
+    const int n = M > 2 ? M : 2;
+    for (int m = blockIdx.x * blockDim.x + threadIdx.x; m < n; m += gridDim.x * blockDim.x) {
         uint8_t keep = 0;
-        if ((m & 1) == 0) {
+        double X[3] = {0.0, 0.0, 0.0};
+        if ((m & 1) == 0 && m < M) {
             const int j = lm_new[(size_t)f * K + m];
             const float* p = spos + ((size_t)f * K + j) * 4;
-            double X[3];
             dlt_point_dev(p[0], p[1], p[2], p[3], cal.P1, cal.P2, X);
             keep = !(X[2] < 0) && !(X[2] > 80);
-            float* o = lm_X + ((size_t)f * K + m) * 3;
-            o[0] = (float)X[0]; o[1] = (float)X[1]; o[2] = (float)X[2];
             if (keep) atomicMax(lm_rows + f, m + 1);
         }
+        float* o = lm_X + ((size_t)f * K + m) * 3;
+        o[0] = keep ? (float)X[0] : 0.0f; o[1] = keep ? (float)X[1] : 0.0f; o[2] = keep ? (float)X[2] : 0.0f;
         lm_keep[(size_t)f * K + m] = keep;
     }
 }

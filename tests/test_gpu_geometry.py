@@ -206,6 +206,9 @@ def test_sequence_pipelined_bit_exact(vo, oracle, syn, seq, calib, depth):
     outs = run()
     X, keep = ctx.get_landmark_rows()
     assert np.array_equal(vo.landmarks_to_world_frames(outs["pose"], outs["n_landmarks"], X, keep), rlm)
+    # the camera-frame rows themselves, zero rows included, are the oracle's
+    _, (oX, okeep) = oracle.run_sequence(L, R, syn.KITTI00_P0, syn.KITTI00_P1, camera_rows=True)
+    assert np.array_equal(keep.astype(bool), okeep.astype(bool)) and X.tobytes() == np.ascontiguousarray(oX, np.float32).tobytes()
     ctx.set_landmark_frame(False)
     # pipeline rules: at most VO_STEP_DEPTH (3) batches pending, other calls refused meanwhile
     ctx.reset()
