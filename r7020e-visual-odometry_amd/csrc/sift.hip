@@ -102,6 +102,9 @@ SiftBuffers sift_view(const SiftBuffers& b, const Pyramid& py, int img0, int n)
     v.kpi = b.kpi + (size_t)img0 * b.kp_cap;
     v.desc = b.desc + (size_t)img0 * b.kp_cap * VO_DESC_LEN;
     v.meta = b.meta + (size_t)img0 * b.kp_cap;
+    v.n_stage = b.n_stage + img0;
+    v.sdesc = b.sdesc + (size_t)img0 * b.kp_cap * VO_DESC_LEN;
+    v.smeta = b.smeta + (size_t)img0 * b.kp_cap;
     v.n_img = n;
     return v;
 }
@@ -127,12 +130,16 @@ hipError_t sift_alloc(SiftBuffers& b, const Pyramid& py, int kp_cap, int cand_ca
     VO_ALLOC(b.kpi, sizeof(KpInt) * (size_t)kp_cap * n);
     VO_ALLOC(b.desc, (size_t)VO_DESC_LEN * kp_cap * n);
     VO_ALLOC(b.meta, sizeof(DescMeta) * (size_t)kp_cap * n);
+    VO_ALLOC(b.n_stage, sizeof(int) * n);
+    VO_ALLOC(b.sdesc, (size_t)VO_DESC_LEN * kp_cap * n);
+    VO_ALLOC(b.smeta, sizeof(DescMeta) * (size_t)kp_cap * n);
 #undef VO_ALLOC
     return hipSuccess;
 }
 
 void sift_free(SiftBuffers& b)
 {
+    hipFree(b.n_stage); hipFree(b.sdesc); hipFree(b.smeta);
     hipFree(b.arena); hipFree(b.tmp); hipFree(b.mask); hipFree(b.woff); hipFree(b.cand); hipFree(b.n_cand); hipFree(b.acc); hipFree(b.n_acc);
     hipFree(b.cout); hipFree(b.koff); hipFree(b.n_kp); hipFree(b.kp); hipFree(b.kpi); hipFree(b.desc); hipFree(b.meta);
     b = SiftBuffers();
@@ -1371,9 +1378,10 @@ __global__ __launch_bounds__(256) void k_seg_count(const unsigned long long* __r
 }
 
 __global__ __launch_bounds__(1024) void k_seg_scan(uint32_t* __restrict__ segc, int* __restrict__ n_cand, int* __restrict__ n_acc,
-                                                   int nseg)
+                                                   int* __restrict__ n_stage, int nseg)
 {
     if (threadIdx.x == 0) n_acc[blockIdx.x] = 0;           // k_refine appends this image's accepted candidates
+    if (threadIdx.x == 0) n_stage[blockIdx.x] = 0;         // k_orient_desc's descriptor slots
     __shared__ uint32_t sh[32];
     const int img = blockIdx.x, tid = threadIdx.x;
     uint32_t v = tid < nseg ? segc[(size_t)img * nseg + tid] : 0u;
@@ -1756,6 +1764,125 @@ __device__ __forceinline__ uint32_t desc_fxq(float v)
 #ifndef VO_ORIENT_WAVES
 #define VO_ORIENT_WAVES 1
 #endif
+// The orientation assignment of one accepted candidate by the whole wave (k_orient's body; also
+// the first half of k_orient_desc): histogram, smoothing, peaks; writes out->ang[0..npk),
+// out->npk and *knpk_slot (and pang[] in LDS when given).  Returns npk (wave-uniform).
+template <int HS>
+__device__ __forceinline__ int orient_candidate(const Pyramid* __restrict__ py, const float* __restrict__ arena, CandOut* out,
+                                                uint32_t* knpk_slot, int img, uint32_t* hp, float* tf, float* hs, float* pang)
+{
+    constexpr int NC = VO_ORIENT_COLS;
+    const int lane = threadIdx.x;
+    const int o = __builtin_amdgcn_readfirstlane(out->o), layer = __builtin_amdgcn_readfirstlane(out->layer);
+    const int r = __builtin_amdgcn_readfirstlane(out->r), c = __builtin_amdgcn_readfirstlane(out->c);
+    const float scl = out->scl;
+    const OctGeom& g = py->oct[o];
+    const int rows = g.rows, cols = g.cols, P = g.pitch;
+    // ---- orientation histogram ----
+    const float* gim = arena + g.g_off[layer] + img * py->istride;
+    const int radius = vo_round(VO_SIFT_ORI_RADIUS * scl);
+    const float sigw = VO_SIFT_ORI_SIG * scl;
+    const float expf_scale = -1.0f / (2.0f * sigw * sigw);
+    typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int b2 = 4 * lane; b2 < HS * NC; b2 += 256) *reinterpret_cast<u4_t*>(&hp[b2]) = u4_t{0u, 0u, 0u, 0u};
+    __syncthreads();
+#if defined(VO_ORIENT_DIAG)
+    const int side = 2 * radius + 1, nsamp = 0;  // diagnostic build (timing only): no sample loop
+#else
+    const int side = 2 * radius + 1, nsamp = side * side;
+#endif
+    const float inv_side = 1.0f / (float)side;          // (s + 0.5) * inv_side is exact enough to floor (s < 2^22)
+    // gradient loads through a buffer resource based at gim - P - 1: one 32-bit lane offset
+    // (the window row as a 24-bit multiply of the clamped row step), row y as one 12-B load
+    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)(gim - P - 1), 0, 0x7FFFFFF0, 0x00020000);
+    const int c_off = r * P + c;                      // wave-uniform
+    constexpr int U = 4;
+    for (int s0 = lane; s0 < nsamp; s0 += 64 * U) {
+        float gx[U], gy[U];
+        int ii[U], jj[U];
+        bool okk[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {                 // indices, bounds, gradient loads
+            const int s = s0 + 64 * q;
+            const float sf = (float)s, iqf = truncf((sf + 0.5f) * inv_side);
+            const int i = (int)iqf - radius, j = (int)(sf - iqf * (float)side) - radius;   // exact: < 2^24
+            const int y = r + i, x = c + j;
+            ii[q] = i; jj[q] = j;
+            okk[q] = (s < nsamp) & (y > 0) & (y < rows - 1) & (x > 0) & (x < cols - 1);
+            // every lane loads (clamped to the interior, weight masked below): no branches
+            const int ic = min(max(i, 1 - r), rows - 2 - r), jc = min(max(j, 1 - c), cols - 2 - c);
+            const int vo = 4 * (c_off + __mul24(ic, P) + jc);
+            typedef int i3_t __attribute__((ext_vector_type(3)));
+            const i3_t h = __builtin_amdgcn_raw_buffer_load_b96(grs, vo, 4 * P, 0);
+            gx[q] = __int_as_float(h.z) - __int_as_float(h.x);
+            gy[q] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 0, 0)) -
+                    __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 8 * P, 0));
+        }
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            const float dx = gx[q], dy = gy[q];
+            // one exp of the combined argument (i^2 + j^2 exact in float); a separable table
+            // (vo_sift_wt, as k_desc uses) measured slower here: 0.60 vs 0.55 ms isolated -- its
+            // two dependent LDS reads per sample cost more than the exp (profiles/r04_d_*)
+            const float fi = (float)ii[q], fj = (float)jj[q];
+            const float w = vo_expf_nonpos((fi * fi + fj * fj) * expf_scale);   // arg in [-21, 0]
+            float mag = vo_grad_mag(dx, dy);
+            float ori = vo_atan2_deg(dy, dx);
+            int bin = vo_round((float)VO_SIFT_ORI_BINS / 360.0f * ori);   // ori in [0, 360): bin in [0, 36]
+            if (bin >= VO_SIFT_ORI_BINS) bin -= VO_SIFT_ORI_BINS;
+            const uint32_t qv = desc_fxq((w * mag) * VO_DESC_FX_SCALE);
+            // private column, bank = lane; masked samples add 0; a returnless LDS add, so the
+            // update does not wait for the column's old value
+            atomicAdd(&hp[bin * NC + (lane & (NC - 1))], okk[q] ? qv : 0u);
+        }
+    }
+    __syncthreads();
+    if (lane < VO_SIFT_ORI_BINS) {
+        uint64_t acc = 0;                             // bin = lane; step q reads column (q + lane) mod NC
+        for (int q = 0; q < NC; ++q) acc += hp[lane * NC + ((q + lane) & (NC - 1))];
+        tf[lane] = vo_hist_fx_to_float(acc);
+    }
+    __syncthreads();
+    const int n = VO_SIFT_ORI_BINS;
+    float hv = -INFINITY;
+    if (lane < n) {
+        float m2 = tf[(lane + n - 2) % n], m1 = tf[(lane + n - 1) % n], p1 = tf[(lane + 1) % n], p2 = tf[(lane + 2) % n];
+        hv = (m2 + p2) * (1.0f / 16.0f) + (m1 + p1) * (4.0f / 16.0f) + tf[lane] * (6.0f / 16.0f);
+        hs[lane] = hv;
+    }
+    const float mx = wave_max(hv);
+    __syncthreads();
+    const float mag_thr = mx * VO_SIFT_ORI_PEAK;
+    bool pk = false;
+    float ang = 0.0f;
+    if (lane < n) {
+        const int l = lane > 0 ? lane - 1 : n - 1, r2 = lane < n - 1 ? lane + 1 : 0;
+        const float hl = hs[l], hr = hs[r2];
+        if (hv > hl && hv > hr && hv >= mag_thr) {
+            pk = true;
+            float bin = (float)lane + 0.5f * (hl - hr) / (hl - 2.0f * hv + hr);
+            bin = bin < 0 ? (float)n + bin : bin >= (float)n ? bin - (float)n : bin;
+            ang = 360.0f - (360.0f / (float)n) * bin;
+            if (fabsf(ang - 360.0f) < VO_FLT_EPSILON) ang = 0.0f;
+        }
+    }
+    const unsigned long long bal = __ballot(pk);
+    if (pk) {
+        const int rank = __popcll(bal & ((1ull << lane) - 1ull));
+        out->ang[rank] = ang;
+        if (pang) pang[rank] = ang;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        out->npk = __popcll(bal);
+#if VO_NPK_COMPACT
+        *knpk_slot = (uint32_t)__popcll(bal);
+#endif
+    }
+    return __popcll(bal);
+}
+
 template <int HS>
 __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                                const int* __restrict__ n_acc, const int* __restrict__ acc,
@@ -1767,7 +1894,6 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
     __shared__ __attribute__((aligned(16))) uint32_t hp[HS * NC];
     __shared__ float tf[VO_SIFT_ORI_BINS];
     __shared__ float hs[VO_SIFT_ORI_BINS];
-    const int lane = threadIdx.x;
     extern __shared__ int fpre[];                    // n_img + 1 ints (dynamic: sized by the launch)
     const long total = flat_setup(n_acc, cand_cap, n_img, fpre);
     for (long t = blockIdx.x; t < total; t += gridDim.x) {
@@ -1780,112 +1906,7 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
 #endif
         CandOut* out = cout + (size_t)img * cand_cap + kidx;
         if (!VO_ACC_LIST && __builtin_amdgcn_readfirstlane(out->npk) != -1) continue;
-        const int o = __builtin_amdgcn_readfirstlane(out->o), layer = __builtin_amdgcn_readfirstlane(out->layer);
-        const int r = __builtin_amdgcn_readfirstlane(out->r), c = __builtin_amdgcn_readfirstlane(out->c);
-        const float scl = out->scl;
-        const OctGeom& g = py->oct[o];
-        const int rows = g.rows, cols = g.cols, P = g.pitch;
-        // ---- orientation histogram ----
-        const float* gim = arena + g.g_off[layer] + img * py->istride;
-        const int radius = vo_round(VO_SIFT_ORI_RADIUS * scl);
-        const float sigw = VO_SIFT_ORI_SIG * scl;
-        const float expf_scale = -1.0f / (2.0f * sigw * sigw);
-        typedef uint32_t u4_t __attribute__((ext_vector_type(4)));
-#pragma unroll
-        for (int b2 = 4 * lane; b2 < HS * NC; b2 += 256) *reinterpret_cast<u4_t*>(&hp[b2]) = u4_t{0u, 0u, 0u, 0u};
-        __syncthreads();
-#if defined(VO_ORIENT_DIAG)
-        const int side = 2 * radius + 1, nsamp = 0;  // diagnostic build (timing only): no sample loop
-#else
-        const int side = 2 * radius + 1, nsamp = side * side;
-#endif
-        const float inv_side = 1.0f / (float)side;          // (s + 0.5) * inv_side is exact enough to floor (s < 2^22)
-        // gradient loads through a buffer resource based at gim - P - 1: one 32-bit lane offset
-        // (the window row as a 24-bit multiply of the clamped row step), row y as one 12-B load
-        const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)(gim - P - 1), 0, 0x7FFFFFF0, 0x00020000);
-        const int c_off = r * P + c;                      // wave-uniform
-        constexpr int U = 4;
-        for (int s0 = lane; s0 < nsamp; s0 += 64 * U) {
-            float gx[U], gy[U];
-            int ii[U], jj[U];
-            bool okk[U];
-#pragma unroll
-            for (int q = 0; q < U; ++q) {                 // indices, bounds, gradient loads
-                const int s = s0 + 64 * q;
-                const float sf = (float)s, iqf = truncf((sf + 0.5f) * inv_side);
-                const int i = (int)iqf - radius, j = (int)(sf - iqf * (float)side) - radius;   // exact: < 2^24
-                const int y = r + i, x = c + j;
-                ii[q] = i; jj[q] = j;
-                okk[q] = (s < nsamp) & (y > 0) & (y < rows - 1) & (x > 0) & (x < cols - 1);
-                // every lane loads (clamped to the interior, weight masked below): no branches
-                const int ic = min(max(i, 1 - r), rows - 2 - r), jc = min(max(j, 1 - c), cols - 2 - c);
-                const int vo = 4 * (c_off + __mul24(ic, P) + jc);
-                typedef int i3_t __attribute__((ext_vector_type(3)));
-                const i3_t h = __builtin_amdgcn_raw_buffer_load_b96(grs, vo, 4 * P, 0);
-                gx[q] = __int_as_float(h.z) - __int_as_float(h.x);
-                gy[q] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 0, 0)) -
-                        __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 8 * P, 0));
-            }
-#pragma unroll
-            for (int q = 0; q < U; ++q) {
-                const float dx = gx[q], dy = gy[q];
-                // one exp of the combined argument (i^2 + j^2 exact in float); a separable table
-                // (vo_sift_wt, as k_desc uses) measured slower here: 0.60 vs 0.55 ms isolated -- its
-                // two dependent LDS reads per sample cost more than the exp (profiles/r04_d_*)
-                const float fi = (float)ii[q], fj = (float)jj[q];
-                const float w = vo_expf_nonpos((fi * fi + fj * fj) * expf_scale);   // arg in [-21, 0]
-                float mag = vo_grad_mag(dx, dy);
-                float ori = vo_atan2_deg(dy, dx);
-                int bin = vo_round((float)VO_SIFT_ORI_BINS / 360.0f * ori);   // ori in [0, 360): bin in [0, 36]
-                if (bin >= VO_SIFT_ORI_BINS) bin -= VO_SIFT_ORI_BINS;
-                const uint32_t qv = desc_fxq((w * mag) * VO_DESC_FX_SCALE);
-                // private column, bank = lane; masked samples add 0; a returnless LDS add, so the
-                // update does not wait for the column's old value
-                atomicAdd(&hp[bin * NC + (lane & (NC - 1))], okk[q] ? qv : 0u);
-            }
-        }
-        __syncthreads();
-        if (lane < VO_SIFT_ORI_BINS) {
-            uint64_t acc = 0;                             // bin = lane; step q reads column (q + lane) mod NC
-            for (int q = 0; q < NC; ++q) acc += hp[lane * NC + ((q + lane) & (NC - 1))];
-            tf[lane] = vo_hist_fx_to_float(acc);
-        }
-        __syncthreads();
-        const int n = VO_SIFT_ORI_BINS;
-        float hv = -INFINITY;
-        if (lane < n) {
-            float m2 = tf[(lane + n - 2) % n], m1 = tf[(lane + n - 1) % n], p1 = tf[(lane + 1) % n], p2 = tf[(lane + 2) % n];
-            hv = (m2 + p2) * (1.0f / 16.0f) + (m1 + p1) * (4.0f / 16.0f) + tf[lane] * (6.0f / 16.0f);
-            hs[lane] = hv;
-        }
-        const float mx = wave_max(hv);
-        __syncthreads();
-        const float mag_thr = mx * VO_SIFT_ORI_PEAK;
-        bool pk = false;
-        float ang = 0.0f;
-        if (lane < n) {
-            const int l = lane > 0 ? lane - 1 : n - 1, r2 = lane < n - 1 ? lane + 1 : 0;
-            const float hl = hs[l], hr = hs[r2];
-            if (hv > hl && hv > hr && hv >= mag_thr) {
-                pk = true;
-                float bin = (float)lane + 0.5f * (hl - hr) / (hl - 2.0f * hv + hr);
-                bin = bin < 0 ? (float)n + bin : bin >= (float)n ? bin - (float)n : bin;
-                ang = 360.0f - (360.0f / (float)n) * bin;
-                if (fabsf(ang - 360.0f) < VO_FLT_EPSILON) ang = 0.0f;
-            }
-        }
-        const unsigned long long bal = __ballot(pk);
-        if (pk) {
-            const int rank = __popcll(bal & ((1ull << lane) - 1ull));
-            out->ang[rank] = ang;
-        }
-        __syncthreads();
-        if (lane == 0) {
-            out->npk = __popcll(bal);
-#if VO_NPK_COMPACT
-            knpk[(size_t)img * cand_cap + kidx] = (uint32_t)__popcll(bal);
-#endif
-        }
+        orient_candidate<HS>(py, arena, out, knpk + (size_t)img * cand_cap + kidx, img, hp, tf, hs, nullptr);
     }
 }
 
@@ -1921,9 +1942,13 @@ __global__ __launch_bounds__(1024) void k_scan_cands(const CandOut* __restrict__
 
 // one thread per accepted candidate (k_refine's list; each writes its own keypoint slots, so the
 // list order does not matter)
+// With `sdesc` (k_orient_desc ran): the candidate's staged descriptors (CandOut.pad0 + p) move to
+// their keypoint rows (desc, meta) and no KpInt records are written.
 __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict__ n_acc, const int* __restrict__ acc,
                          const uint32_t* __restrict__ koff, vo_keypoint* __restrict__ kp, KpInt* __restrict__ kpi,
-                         int cand_cap, int kp_cap, int n_img, int upsample)
+                         int cand_cap, int kp_cap, int n_img, int upsample,
+                         const uint8_t* __restrict__ sdesc, const DescMeta* __restrict__ smeta,
+                         uint8_t* __restrict__ desc, DescMeta* __restrict__ meta)
 {
     __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
     const long total = flat_setup(n_acc, cand_cap, n_img, fpre);
@@ -1951,10 +1976,28 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
             q.layer = co.layer;
             q.scale = co.scl * oscale;
             kp[(size_t)img * kp_cap + idx] = q;
-            KpInt qi;
-            qi.xo = co.xo; qi.yo = co.yo; qi.scl = co.scl; qi.angle = co.ang[p];
-            qi.o = co.o; qi.layer = co.layer; qi.pad0 = 0; qi.pad1 = 0;
-            kpi[(size_t)img * kp_cap + idx] = qi;
+            if (sdesc) {
+                // the staged row (a permutation of the image's keypoints); past max_keypoints (the
+                // flagged overflow, VO_FLAG_KEYPOINTS) it was not computed: a zero descriptor
+                const uint32_t src = (uint32_t)co.pad0 + p;
+                typedef uint32_t u4c_t __attribute__((ext_vector_type(4)));
+                u4c_t* d4 = reinterpret_cast<u4c_t*>(desc + ((size_t)img * kp_cap + idx) * VO_DESC_LEN);
+                if (src < (uint32_t)kp_cap) {
+                    const u4c_t* s4 = reinterpret_cast<const u4c_t*>(sdesc + ((size_t)img * kp_cap + src) * VO_DESC_LEN);
+#pragma unroll
+                    for (int w = 0; w < VO_DESC_LEN / 16; ++w) d4[w] = s4[w];
+                    meta[(size_t)img * kp_cap + idx] = smeta[(size_t)img * kp_cap + src];
+                } else {
+#pragma unroll
+                    for (int w = 0; w < VO_DESC_LEN / 16; ++w) d4[w] = u4c_t{0u, 0u, 0u, 0u};
+                    meta[(size_t)img * kp_cap + idx] = DescMeta{0, 0.0f};
+                }
+            } else {
+                KpInt qi;
+                qi.xo = co.xo; qi.yo = co.yo; qi.scl = co.scl; qi.angle = co.ang[p];
+                qi.o = co.o; qi.layer = co.layer; qi.pad0 = 0; qi.pad1 = 0;
+                kpi[(size_t)img * kp_cap + idx] = qi;
+            }
         }
     }
 }
@@ -1984,6 +2027,9 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
 #endif
 #ifndef VO_DESC_U
 #define VO_DESC_U 2               // blocks of 64 samples per batch
+#endif
+#ifndef VO_ORIENT_DESC
+#define VO_ORIENT_DESC 1          // 0: k_orient, k_desc as separate passes (the window fetched twice)
 #endif
 // The keypoint's descriptor window tables into LDS (hdr, rtab, wtab; layout of dt_stride): its rotation,
 // radius, sample count, row table -- each window row i's column interval [jlo, jhi] inside the
@@ -2096,6 +2142,192 @@ __device__ __forceinline__ void desc_tables(const Pyramid* __restrict__ py, KpIn
     __syncthreads();
 }
 
+// The descriptor of one keypoint by the whole wave (k_desc's body; also the second half of
+// k_orient_desc): window tables, sample loop, histogram fold, normalisation, u8 quantisation;
+// writes dst[0..128) and *mdst.  hfx: DCOPIES * DCS words of LDS; dyn: dt_stride(dcap) words.
+template <int DCOPIES>
+__device__ __forceinline__ void desc_keypoint(const Pyramid* __restrict__ py, const float* __restrict__ arena, const KpInt q,
+                                              int img, int dcap, uint32_t* hfx, uint32_t* dyn, uint8_t* dst, DescMeta* mdst)
+{
+    const int lane = threadIdx.x;
+    const float bins_per_deg = (float)DN / 360.0f;
+    static_assert((DCOPIES * DCS) % 4 == 0, "16-B zeroing");
+    typedef uint32_t u4z_t __attribute__((ext_vector_type(4)));
+    for (int b = 4 * lane; b < DCOPIES * DCS; b += 256) *reinterpret_cast<u4z_t*>(&hfx[b]) = u4z_t{0u, 0u, 0u, 0u};
+    desc_tables(py, q, dcap, dyn, dyn + dt_rtab_off(), reinterpret_cast<float*>(dyn + dt_wtab_off(dcap)), lane);
+    const uint32_t* const hdr = dyn;
+    const uint32_t* const rtab = dyn + dt_rtab_off();
+    const float* const wtab = reinterpret_cast<const float*>(dyn + dt_wtab_off(dcap));
+    const int o = __builtin_amdgcn_readfirstlane((int)hdr[DT_O]), layer = __builtin_amdgcn_readfirstlane((int)hdr[DT_LAYER]);
+    const OctGeom& g = py->oct[o];
+    const int P = g.pitch;
+    const float* gim = arena + g.g_off[layer] + img * py->istride;
+    const float ori = __uint_as_float(hdr[DT_ORI]);
+    const int px = (int)hdr[DT_PX], pyy = (int)hdr[DT_PY], radius = (int)hdr[DT_RADIUS];
+    const float cos_t = __uint_as_float(hdr[DT_COS]), sin_t = __uint_as_float(hdr[DT_SIN]);
+#if defined(VO_DESC_DIAG) && VO_DESC_DIAG >= 1
+    const int nsamp = 0;                         // diagnostic build (timing only): no sample loop
+#else
+    const int nsamp = (int)hdr[DT_NSAMP];
+#endif
+    uint32_t* hc = hfx + (lane & (DCOPIES - 1)) * DCS;
+    // one sample: weights, bins, fixed-point LDS atomics
+    auto accum = [&](float c_rot, float r_rot, float w, float dx, float dy) {
+        float rbin = r_rot + (float)(DW / 2) - 0.5f;
+        float cbin = c_rot + (float)(DW / 2) - 0.5f;
+        float ang = vo_atan2_deg(dy, dx);
+        float mag = vo_grad_mag(dx, dy) * w;         // = (|grad| w_ij) 2^10 exactly (w from the x 32 table)
+        float obin = (ang - ori) * bins_per_deg;
+        // floors kept in float ((float)(int)floorf(v) == floorf(v) here); the cell index is an
+        // exact small-integer float expression, one conversion; obin in [-8, 8] so the circular
+        // wrap of o0 is a mask (DN = 8)
+        const float fr0 = floorf(rbin), fc0 = floorf(cbin), fo0 = floorf(obin);
+        rbin -= fr0; cbin -= fc0; obin -= fo0;
+        const int o0 = (int)fo0 & (DN - 1);
+        // histogram word of cell (fr0 + 1, fc0 + 1): ((fr0 + 1) (DW + 2) + fc0 + 1) DBS as two
+        // exact small-integer fmas (< 2^24), one conversion
+        const float cell_w = fmaf(fr0, (float)((DW + 2) * DBS), fmaf(fc0, (float)DBS, (float)((DW + 3) * DBS)));
+        float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+        float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+        float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+        float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+        float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+        float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+        float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+        uint32_t* h = hc + (int)cell_w + o0;
+        atomicAdd(h, desc_fxq(v_rco000));
+        atomicAdd(h + 1, desc_fxq(v_rco001));
+        atomicAdd(h + DBS, desc_fxq(v_rco010));
+        atomicAdd(h + DBS + 1, desc_fxq(v_rco011));
+        atomicAdd(h + (DW + 2) * DBS, desc_fxq(v_rco100));
+        atomicAdd(h + (DW + 2) * DBS + 1, desc_fxq(v_rco101));
+        atomicAdd(h + (DW + 3) * DBS, desc_fxq(v_rco110));
+        atomicAdd(h + (DW + 3) * DBS + 1, desc_fxq(v_rco111));
+    };
+    // the gradient neighbours of a listed sample (every listed sample is interior): x+1, x-1 as
+    // one 12-B load (through a 3-float type declared with the 4-B alignment the address has),
+    // y-1, y+1
+    // buffer loads with one 32-bit lane offset: the resource starts at the sample's row y-1
+    // column x-1 for offset 0 (gim - P - 1), so row y-1 is +4 B, row y (x-1..x+1) +4P B and
+    // row y+1 +8P + 4 B -- no 64-bit address arithmetic per sample; the row offset is a
+    // 24-bit multiply (|i| <= RMAX, P < 2^23)
+    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)(gim - P - 1), 0, 0x7FFFFFF0, 0x00020000);
+    const int c_off = pyy * P + px;                  // wave-uniform
+    auto grad_loads = [&](int i, int j, float* g4) {
+        const int vo = 4 * (c_off + __mul24(i, P) + j);
+        typedef int i3_t __attribute__((ext_vector_type(3)));
+        const i3_t h = __builtin_amdgcn_raw_buffer_load_b96(grs, vo, 4 * P, 0);
+        g4[0] = __int_as_float(h.z); g4[1] = __int_as_float(h.x);
+        g4[2] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 0, 0));
+        g4[3] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 8 * P, 0));
+    };
+    {   // Block lookup: the 64 samples bs .. bs+63 of a block start in row rb (wave-uniform) and
+        // span a few rows; every lane reads the same K+2 table entries (LDS broadcast, one round
+        // trip) and selects its row by comparing its sample index with the row starts -- no
+        // per-lane walk, no dependent LDS chain.  Rows past rb+K (short rows at a rotated
+        // window's corners, rows of zero length above the image) take another round.
+        // The gradient loads of the next U blocks are issued before the current U blocks are
+        // accumulated (two slot sets, a pair of batches per loop iteration; the loads of a
+        // batch past the window are clamped to its last sample, so every iteration issues
+        // the same loads and the wait counts stay exact).
+        constexpr int U = VO_DESC_U, K = 4;
+        int rb = 0;                                      // wave-uniform row of the next block's first sample
+        auto locate = [&](int bs, int& i_o, int& j_o) {
+            const int sc = min(bs + lane, nsamp - 1), last = min(bs + 63, nsamp - 1);
+            uint32_t sel = rtab[rb];
+            int row = rb;
+            for (;;) {
+                const uint32_t* tb = rtab + rb;
+                uint32_t e[K + 2];
+#pragma unroll
+                for (int k = 1; k <= K + 1; ++k) e[k] = tb[k];
+#pragma unroll
+                for (int k = 1; k <= K; ++k) {
+                    const bool c = (int)(e[k] & 0xFFFFu) <= sc;
+                    sel = c ? e[k] : sel;
+                    row += c ? 1 : 0;
+                }
+                if ((int)(e[K + 1] & 0xFFFFu) > last) break;   // uniform: every lane's row found
+                rb += K;
+            }
+            i_o = row - radius;
+            j_o = ((int)sel >> 16) + (sc - (int)(sel & 0xFFFFu));
+            rb = __builtin_amdgcn_readlane(row, 63);
+        };
+        struct Slot { float g[4]; int i, j; };
+        auto issue = [&](int sb, Slot (&S)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) locate(sb + 64 * u, S[u].i, S[u].j);
+#pragma unroll
+            for (int u = 0; u < U; ++u) grad_loads(S[u].i, S[u].j, S[u].g);
+        };
+        auto consume = [&](int sb, const Slot (&S)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (sb + 64 * u + lane < nsamp) {
+                    const float fi = (float)S[u].i, fj = (float)S[u].j;
+                    accum(fj * cos_t - fi * sin_t, fj * sin_t + fi * cos_t, wtab[abs(S[u].i)] * wtab[abs(S[u].j)],
+                          S[u].g[0] - S[u].g[1], S[u].g[2] - S[u].g[3]);
+                }
+            }
+        };
+        if (nsamp > 0) {
+            Slot A[U], B[U];
+            int sb = 0;
+            issue(0, A);
+            for (;;) {
+                issue(sb + 64 * U, B);
+                consume(sb, A);
+                sb += 64 * U;
+                if (sb >= nsamp) break;
+                issue(sb + 64 * U, A);
+                consume(sb, B);
+                sb += 64 * U;
+                if (sb >= nsamp) break;
+            }
+        }
+    }
+    __syncthreads();
+    // fold the circular orientation bins and convert; lane holds dst[lane], dst[lane+64]
+    float dv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int kk = lane + 64 * h;
+        const int cell = kk / DN, ob = kk - cell * DN;
+        const int ci = cell / DW, cj = cell - ci * DW;
+        const int base = ((ci + 1) * (DW + 2) + (cj + 1)) * DBS;
+        uint32_t v = 0;
+#pragma unroll
+        for (int cp = 0; cp < DCOPIES; ++cp) {
+            v += hfx[cp * DCS + base + ob];
+            if (ob == 0) v += hfx[cp * DCS + base + DN];
+        }
+        dv[h] = vo_desc_fx_to_float(v);
+    }
+    const float nrm0 = wave_tree_sum(dv[0] * dv[0] + dv[1] * dv[1]);
+    const float thr = sqrtf(nrm0) * VO_SIFT_DESCR_MAG_THR;
+    dv[0] = dv[0] < thr ? dv[0] : thr;
+    dv[1] = dv[1] < thr ? dv[1] : thr;
+    const float nrm = sqrtf(wave_tree_sum(dv[0] * dv[0] + dv[1] * dv[1]));
+    const float scale = VO_SIFT_DESCR_INT_FCTR / (nrm > VO_FLT_EPSILON ? nrm : VO_FLT_EPSILON);
+    int qv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        float v = rintf(dv[h] * scale);
+        qv[h] = v < 0.0f ? 0 : v > 255.0f ? 255 : (int)v;
+    }
+    dst[lane] = (uint8_t)qv[0];
+    dst[lane + 64] = (uint8_t)qv[1];
+    const int sum = wave_tree_sum(qv[0] + qv[1]), sq = wave_tree_sum(qv[0] * qv[0] + qv[1] * qv[1]);
+    if (lane == 0) {
+        DescMeta m;
+        m.sum = sum;
+        m.inv_norm = sq > 0 ? 1.0f / sqrtf((float)sq) : 0.0f;
+        *mdst = m;
+    }
+    __syncthreads();
+}
+
 template <int DCOPIES>
 __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
                                              const KpInt* __restrict__ kpi, const int* __restrict__ n_kp,
@@ -2113,190 +2345,71 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
     // one-wave workgroups leave LDS for the scale-space waves that share their CUs.
     extern __shared__ uint32_t dyn[];
     const int dcap = py->dcap, ts = dt_stride(dcap);
-    const uint32_t* const hdr = dyn;
-    const uint32_t* const rtab = dyn + dt_rtab_off();
-    const float* const wtab = reinterpret_cast<const float*>(dyn + dt_wtab_off(dcap));
     int* const fpre = reinterpret_cast<int*>(dyn + ts);
-    const int lane = threadIdx.x;
     const long total = flat_setup(n_kp, kp_cap, n_img, fpre);
-    const float bins_per_deg = (float)DN / 360.0f;
     for (long t = blockIdx.x; t < total; t += gridDim.x) {
         int img, k;
         flat_find_wave(fpre, n_img, t, img, k);
         const KpInt q = kpi[(size_t)img * kp_cap + k];
-        static_assert((DCOPIES * DCS) % 4 == 0, "16-B zeroing");
-        typedef uint32_t u4z_t __attribute__((ext_vector_type(4)));
-        for (int b = 4 * lane; b < DCOPIES * DCS; b += 256) *reinterpret_cast<u4z_t*>(&hfx[b]) = u4z_t{0u, 0u, 0u, 0u};
-        desc_tables(py, q, dcap, dyn, dyn + dt_rtab_off(), reinterpret_cast<float*>(dyn + dt_wtab_off(dcap)), lane);
-        const int o = __builtin_amdgcn_readfirstlane((int)hdr[DT_O]), layer = __builtin_amdgcn_readfirstlane((int)hdr[DT_LAYER]);
-        const OctGeom& g = py->oct[o];
-        const int P = g.pitch;
-        const float* gim = arena + g.g_off[layer] + img * py->istride;
-        const float ori = __uint_as_float(hdr[DT_ORI]);
-        const int px = (int)hdr[DT_PX], pyy = (int)hdr[DT_PY], radius = (int)hdr[DT_RADIUS];
-        const float cos_t = __uint_as_float(hdr[DT_COS]), sin_t = __uint_as_float(hdr[DT_SIN]);
-#if defined(VO_DESC_DIAG) && VO_DESC_DIAG >= 1
-        const int nsamp = 0;                         // diagnostic build (timing only): no sample loop
-#else
-        const int nsamp = (int)hdr[DT_NSAMP];
+        desc_keypoint<DCOPIES>(py, arena, q, img, dcap, hfx, dyn, desc + ((size_t)img * kp_cap + k) * VO_DESC_LEN,
+                               meta + (size_t)img * kp_cap + k);
+    }
+}
+
+// Orientation and descriptors in one pass (VO.m:79-84): one wave per accepted candidate runs
+// orient_candidate, takes npk descriptor slots of its image (one atomic), and computes each
+// peak's descriptor (desc_keypoint) into the staging arrays.  The descriptor window of a
+// keypoint holds its orientation window (4.5 sigma < the rotated square's inscribed radius,
+// 7.5 sigma), so the descriptor's gradient loads find those lines in the cache the orientation
+// pass just filled: the window is fetched from HBM once instead of twice (k_orient then k_desc).
+// k_expand then writes the keypoints in candidate / peak order and moves each staged descriptor
+// to its keypoint's row.  The arithmetic of both halves is k_orient's and k_desc's, so every
+// bit is unchanged; slots past max_keypoints (the flagged overflow) are not computed.
+#ifndef VO_OD_WAVES
+#define VO_OD_WAVES 4             // k_orient_desc's register budget, waves per SIMD (5: 96 VGPRs, 40 spilled)
 #endif
-        uint32_t* hc = hfx + (lane & (DCOPIES - 1)) * DCS;
-        // one sample: weights, bins, fixed-point LDS atomics
-        auto accum = [&](float c_rot, float r_rot, float w, float dx, float dy) {
-            float rbin = r_rot + (float)(DW / 2) - 0.5f;
-            float cbin = c_rot + (float)(DW / 2) - 0.5f;
-            float ang = vo_atan2_deg(dy, dx);
-            float mag = vo_grad_mag(dx, dy) * w;         // = (|grad| w_ij) 2^10 exactly (w from the x 32 table)
-            float obin = (ang - ori) * bins_per_deg;
-            // floors kept in float ((float)(int)floorf(v) == floorf(v) here); the cell index is an
-            // exact small-integer float expression, one conversion; obin in [-8, 8] so the circular
-            // wrap of o0 is a mask (DN = 8)
-            const float fr0 = floorf(rbin), fc0 = floorf(cbin), fo0 = floorf(obin);
-            rbin -= fr0; cbin -= fc0; obin -= fo0;
-            const int o0 = (int)fo0 & (DN - 1);
-            // histogram word of cell (fr0 + 1, fc0 + 1): ((fr0 + 1) (DW + 2) + fc0 + 1) DBS as two
-            // exact small-integer fmas (< 2^24), one conversion
-            const float cell_w = fmaf(fr0, (float)((DW + 2) * DBS), fmaf(fc0, (float)DBS, (float)((DW + 3) * DBS)));
-            float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-            float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
-            float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-            float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
-            float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
-            float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
-            float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-            uint32_t* h = hc + (int)cell_w + o0;
-            atomicAdd(h, desc_fxq(v_rco000));
-            atomicAdd(h + 1, desc_fxq(v_rco001));
-            atomicAdd(h + DBS, desc_fxq(v_rco010));
-            atomicAdd(h + DBS + 1, desc_fxq(v_rco011));
-            atomicAdd(h + (DW + 2) * DBS, desc_fxq(v_rco100));
-            atomicAdd(h + (DW + 2) * DBS + 1, desc_fxq(v_rco101));
-            atomicAdd(h + (DW + 3) * DBS, desc_fxq(v_rco110));
-            atomicAdd(h + (DW + 3) * DBS + 1, desc_fxq(v_rco111));
-        };
-        // the gradient neighbours of a listed sample (every listed sample is interior): x+1, x-1 as
-        // one 12-B load (through a 3-float type declared with the 4-B alignment the address has),
-        // y-1, y+1
-        // buffer loads with one 32-bit lane offset: the resource starts at the sample's row y-1
-        // column x-1 for offset 0 (gim - P - 1), so row y-1 is +4 B, row y (x-1..x+1) +4P B and
-        // row y+1 +8P + 4 B -- no 64-bit address arithmetic per sample; the row offset is a
-        // 24-bit multiply (|i| <= RMAX, P < 2^23)
-        const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc((void*)(gim - P - 1), 0, 0x7FFFFFF0, 0x00020000);
-        const int c_off = pyy * P + px;                  // wave-uniform
-        auto grad_loads = [&](int i, int j, float* g4) {
-            const int vo = 4 * (c_off + __mul24(i, P) + j);
-            typedef int i3_t __attribute__((ext_vector_type(3)));
-            const i3_t h = __builtin_amdgcn_raw_buffer_load_b96(grs, vo, 4 * P, 0);
-            g4[0] = __int_as_float(h.z); g4[1] = __int_as_float(h.x);
-            g4[2] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 0, 0));
-            g4[3] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(grs, vo + 4, 8 * P, 0));
-        };
-        {   // Block lookup: the 64 samples bs .. bs+63 of a block start in row rb (wave-uniform) and
-            // span a few rows; every lane reads the same K+2 table entries (LDS broadcast, one round
-            // trip) and selects its row by comparing its sample index with the row starts -- no
-            // per-lane walk, no dependent LDS chain.  Rows past rb+K (short rows at a rotated
-            // window's corners, rows of zero length above the image) take another round.
-            // The gradient loads of the next U blocks are issued before the current U blocks are
-            // accumulated (two slot sets, a pair of batches per loop iteration; the loads of a
-            // batch past the window are clamped to its last sample, so every iteration issues
-            // the same loads and the wait counts stay exact).
-            constexpr int U = VO_DESC_U, K = 4;
-            int rb = 0;                                      // wave-uniform row of the next block's first sample
-            auto locate = [&](int bs, int& i_o, int& j_o) {
-                const int sc = min(bs + lane, nsamp - 1), last = min(bs + 63, nsamp - 1);
-                uint32_t sel = rtab[rb];
-                int row = rb;
-                for (;;) {
-                    const uint32_t* tb = rtab + rb;
-                    uint32_t e[K + 2];
-#pragma unroll
-                    for (int k = 1; k <= K + 1; ++k) e[k] = tb[k];
-#pragma unroll
-                    for (int k = 1; k <= K; ++k) {
-                        const bool c = (int)(e[k] & 0xFFFFu) <= sc;
-                        sel = c ? e[k] : sel;
-                        row += c ? 1 : 0;
-                    }
-                    if ((int)(e[K + 1] & 0xFFFFu) > last) break;   // uniform: every lane's row found
-                    rb += K;
-                }
-                i_o = row - radius;
-                j_o = ((int)sel >> 16) + (sc - (int)(sel & 0xFFFFu));
-                rb = __builtin_amdgcn_readlane(row, 63);
-            };
-            struct Slot { float g[4]; int i, j; };
-            auto issue = [&](int sb, Slot (&S)[U]) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) locate(sb + 64 * u, S[u].i, S[u].j);
-#pragma unroll
-                for (int u = 0; u < U; ++u) grad_loads(S[u].i, S[u].j, S[u].g);
-            };
-            auto consume = [&](int sb, const Slot (&S)[U]) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (sb + 64 * u + lane < nsamp) {
-                        const float fi = (float)S[u].i, fj = (float)S[u].j;
-                        accum(fj * cos_t - fi * sin_t, fj * sin_t + fi * cos_t, wtab[abs(S[u].i)] * wtab[abs(S[u].j)],
-                              S[u].g[0] - S[u].g[1], S[u].g[2] - S[u].g[3]);
-                    }
-                }
-            };
-            if (nsamp > 0) {
-                Slot A[U], B[U];
-                int sb = 0;
-                issue(0, A);
-                for (;;) {
-                    issue(sb + 64 * U, B);
-                    consume(sb, A);
-                    sb += 64 * U;
-                    if (sb >= nsamp) break;
-                    issue(sb + 64 * U, A);
-                    consume(sb, B);
-                    sb += 64 * U;
-                    if (sb >= nsamp) break;
-                }
-            }
+template <int HS, int DCOPIES>
+__global__ __launch_bounds__(64, VO_OD_WAVES) void k_orient_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
+                                                    const int* __restrict__ n_acc, const int* __restrict__ acc,
+                                                    CandOut* __restrict__ cout, uint32_t* __restrict__ knpk,
+                                                    int* __restrict__ n_stage, uint8_t* __restrict__ sdesc,
+                                                    DescMeta* __restrict__ smeta, int cand_cap, int kp_cap, int n_img)
+{
+    constexpr int NC = VO_ORIENT_COLS;
+    static_assert(HS >= VO_SIFT_ORI_BINS && (HS * NC) % 4 == 0 && (NC == 64 || NC == 32 || NC == 16), "columns hold the 36 bins");
+    static_assert(DCS >= DHIST, "copy stride holds a histogram");
+    constexpr int HW = HS * NC > DCOPIES * DCS ? HS * NC : DCOPIES * DCS;
+    __shared__ __attribute__((aligned(16))) uint32_t hbuf[HW];      // orientation histogram, then descriptor copies
+    __shared__ float tf[VO_SIFT_ORI_BINS];
+    __shared__ float hs[VO_SIFT_ORI_BINS];
+    __shared__ float pang[VO_SIFT_MAX_PEAKS];
+    extern __shared__ uint32_t dyn[];                // descriptor tables (dt_stride(dcap)), then the image prefix
+    const int dcap = py->dcap, ts = dt_stride(dcap);
+    int* const fpre = reinterpret_cast<int*>(dyn + ts);
+    const int lane = threadIdx.x;
+    const long total = flat_setup(n_acc, cand_cap, n_img, fpre);
+    for (long t = blockIdx.x; t < total; t += gridDim.x) {
+        int img, a;
+        flat_find_wave(fpre, n_img, t, img, a);
+        const int kidx = __builtin_amdgcn_readfirstlane(acc[(size_t)img * cand_cap + a]);
+        CandOut* out = cout + (size_t)img * cand_cap + kidx;
+        const int npk = __builtin_amdgcn_readfirstlane(
+            orient_candidate<HS>(py, arena, out, knpk + (size_t)img * cand_cap + kidx, img, hbuf, tf, hs, pang));
+        int base = 0;
+        if (lane == 0 && npk > 0) {
+            base = atomicAdd(n_stage + img, npk);
+            out->pad0 = base;                            // k_expand reads the staged rows from here
         }
-        __syncthreads();
-        // fold the circular orientation bins and convert; lane holds dst[lane], dst[lane+64]
-        float dv[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int kk = lane + 64 * h;
-            const int cell = kk / DN, ob = kk - cell * DN;
-            const int ci = cell / DW, cj = cell - ci * DW;
-            const int base = ((ci + 1) * (DW + 2) + (cj + 1)) * DBS;
-            uint32_t v = 0;
-#pragma unroll
-            for (int cp = 0; cp < DCOPIES; ++cp) {
-                v += hfx[cp * DCS + base + ob];
-                if (ob == 0) v += hfx[cp * DCS + base + DN];
-            }
-            dv[h] = vo_desc_fx_to_float(v);
+        base = __builtin_amdgcn_readfirstlane(base);
+        KpInt q;
+        q.xo = out->xo; q.yo = out->yo; q.scl = out->scl;
+        q.o = __builtin_amdgcn_readfirstlane(out->o); q.layer = __builtin_amdgcn_readfirstlane(out->layer);
+        q.pad0 = 0; q.pad1 = 0;
+        for (int p = 0; p < npk && base + p < kp_cap; ++p) {
+            q.angle = pang[p];
+            const size_t row = (size_t)img * kp_cap + base + p;
+            desc_keypoint<DCOPIES>(py, arena, q, img, dcap, hbuf, dyn, sdesc + row * VO_DESC_LEN, smeta + row);
         }
-        const float nrm0 = wave_tree_sum(dv[0] * dv[0] + dv[1] * dv[1]);
-        const float thr = sqrtf(nrm0) * VO_SIFT_DESCR_MAG_THR;
-        dv[0] = dv[0] < thr ? dv[0] : thr;
-        dv[1] = dv[1] < thr ? dv[1] : thr;
-        const float nrm = sqrtf(wave_tree_sum(dv[0] * dv[0] + dv[1] * dv[1]));
-        const float scale = VO_SIFT_DESCR_INT_FCTR / (nrm > VO_FLT_EPSILON ? nrm : VO_FLT_EPSILON);
-        int qv[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            float v = rintf(dv[h] * scale);
-            qv[h] = v < 0.0f ? 0 : v > 255.0f ? 255 : (int)v;
-        }
-        uint8_t* dst = desc + ((size_t)img * kp_cap + k) * VO_DESC_LEN;
-        dst[lane] = (uint8_t)qv[0];
-        dst[lane + 64] = (uint8_t)qv[1];
-        const int sum = wave_tree_sum(qv[0] + qv[1]), sq = wave_tree_sum(qv[0] * qv[0] + qv[1] * qv[1]);
-        if (lane == 0) {
-            DescMeta m;
-            m.sum = sum;
-            m.inv_norm = sq > 0 ? 1.0f / sqrtf((float)sq) : 0.0f;
-            meta[(size_t)img * kp_cap + k] = m;
-        }
-        __syncthreads();
     }
 }
 
@@ -2612,18 +2725,28 @@ void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const v
     float* A = b.arena;
     const dim3 gs(py.n_seg > 0 ? py.n_seg : 1, n_img);
     VO_LAUNCH(k_seg_count, gs, dim3(256), 0, s, b.mask, b.woff, py.n_words, py.n_seg);
-    VO_LAUNCH(k_seg_scan, dim3(n_img), dim3(1024), 0, s, b.woff, b.n_cand, b.n_acc, py.n_seg);
+    VO_LAUNCH(k_seg_scan, dim3(n_img), dim3(1024), 0, s, b.woff, b.n_cand, b.n_acc, b.n_stage, py.n_seg);
     VO_LAUNCH(k_seg_emit, gs, dim3(256), 0, s, d_py, b.mask, (const uint32_t*)b.woff, b.cand, b.cand_cap);
     VO_LAUNCH(k_refine, dim3(VO_REFINE_BLOCKS), dim3(256), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.acc, b.n_acc, b.koff, b.cand_cap, n_img,
               p.contrast_threshold, p.edge_threshold, p.sigma);
     const size_t fpre_bytes = sizeof(int) * (size_t)(n_img + 1);
     const int* n_walk = VO_ACC_LIST ? b.n_acc : b.n_cand;    // the accepted list, or every candidate
+    const size_t dt_bytes = sizeof(uint32_t) * (size_t)dt_stride(py.dcap);
+    if (VO_ORIENT_DESC && VO_ACC_LIST) {
+        // orientation + descriptors in one pass, then the keypoint order
+        VO_LAUNCH_NAMED("k_orient_desc", (k_orient_desc<36, VO_DESC_COPIES>), dim3(kFeatureGrid), dim3(64),
+                        dt_bytes + fpre_bytes, s, d_py, A, n_walk, b.acc, b.cout, b.koff, b.n_stage, b.sdesc, b.smeta,
+                        b.cand_cap, b.kp_cap, n_img);
+        VO_LAUNCH(k_scan_cands, dim3(n_img), dim3(1024), 0, s, b.cout, b.n_cand, b.koff, b.n_kp, b.cand_cap);
+        VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, n_walk, b.acc, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
+                  n_img, p.upsample, b.sdesc, b.smeta, b.desc, b.meta);
+        return;
+    }
     VO_LAUNCH_NAMED("k_orient", (k_orient<36>), dim3(kFeatureGrid), dim3(64), fpre_bytes, s, d_py, A, n_walk, b.acc,
                     b.cout, b.koff, b.cand_cap, n_img);
     VO_LAUNCH(k_scan_cands, dim3(n_img), dim3(1024), 0, s, b.cout, b.n_cand, b.koff, b.n_kp, b.cand_cap);
     VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, n_walk, b.acc, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
-                       n_img, p.upsample);
-    const size_t dt_bytes = sizeof(uint32_t) * (size_t)dt_stride(py.dcap);
+              n_img, p.upsample, (const uint8_t*)nullptr, (const DescMeta*)nullptr, (uint8_t*)nullptr, (DescMeta*)nullptr);
     // 4 histogram copies: 2 -> +4 %, 8 -> +33 % k_desc time (MI355X)
     VO_LAUNCH_NAMED("k_desc", (k_desc<VO_DESC_COPIES>), dim3(kFeatureGrid), dim3(64), dt_bytes + fpre_bytes, s, d_py, A,
                     b.kpi, b.n_kp, b.desc, b.meta, b.kp_cap, n_img);
