@@ -102,9 +102,6 @@ SiftBuffers sift_view(const SiftBuffers& b, const Pyramid& py, int img0, int n)
     v.kpi = b.kpi + (size_t)img0 * b.kp_cap;
     v.desc = b.desc + (size_t)img0 * b.kp_cap * VO_DESC_LEN;
     v.meta = b.meta + (size_t)img0 * b.kp_cap;
-    v.n_stage = b.n_stage + img0;
-    v.sdesc = b.sdesc + (size_t)img0 * b.kp_cap * VO_DESC_LEN;
-    v.smeta = b.smeta + (size_t)img0 * b.kp_cap;
     v.n_img = n;
     return v;
 }
@@ -130,16 +127,12 @@ hipError_t sift_alloc(SiftBuffers& b, const Pyramid& py, int kp_cap, int cand_ca
     VO_ALLOC(b.kpi, sizeof(KpInt) * (size_t)kp_cap * n);
     VO_ALLOC(b.desc, (size_t)VO_DESC_LEN * kp_cap * n);
     VO_ALLOC(b.meta, sizeof(DescMeta) * (size_t)kp_cap * n);
-    VO_ALLOC(b.n_stage, sizeof(int) * n);
-    VO_ALLOC(b.sdesc, (size_t)VO_DESC_LEN * kp_cap * n);
-    VO_ALLOC(b.smeta, sizeof(DescMeta) * (size_t)kp_cap * n);
 #undef VO_ALLOC
     return hipSuccess;
 }
 
 void sift_free(SiftBuffers& b)
 {
-    hipFree(b.n_stage); hipFree(b.sdesc); hipFree(b.smeta);
     hipFree(b.arena); hipFree(b.tmp); hipFree(b.mask); hipFree(b.woff); hipFree(b.cand); hipFree(b.n_cand); hipFree(b.acc); hipFree(b.n_acc);
     hipFree(b.cout); hipFree(b.koff); hipFree(b.n_kp); hipFree(b.kp); hipFree(b.kpi); hipFree(b.desc); hipFree(b.meta);
     b = SiftBuffers();
@@ -1378,10 +1371,9 @@ __global__ __launch_bounds__(256) void k_seg_count(const unsigned long long* __r
 }
 
 __global__ __launch_bounds__(1024) void k_seg_scan(uint32_t* __restrict__ segc, int* __restrict__ n_cand, int* __restrict__ n_acc,
-                                                   int* __restrict__ n_stage, int nseg)
+                                                   int nseg)
 {
     if (threadIdx.x == 0) n_acc[blockIdx.x] = 0;           // k_refine appends this image's accepted candidates
-    if (threadIdx.x == 0) n_stage[blockIdx.x] = 0;         // k_orient_desc's descriptor slots
     __shared__ uint32_t sh[32];
     const int img = blockIdx.x, tid = threadIdx.x;
     uint32_t v = tid < nseg ? segc[(size_t)img * nseg + tid] : 0u;
@@ -1764,12 +1756,12 @@ __device__ __forceinline__ uint32_t desc_fxq(float v)
 #ifndef VO_ORIENT_WAVES
 #define VO_ORIENT_WAVES 1
 #endif
-// The orientation assignment of one accepted candidate by the whole wave (k_orient's body; also
-// the first half of k_orient_desc): histogram, smoothing, peaks; writes out->ang[0..npk),
-// out->npk and *knpk_slot (and pang[] in LDS when given).  Returns npk (wave-uniform).
+// The orientation assignment of one accepted candidate by the whole wave (k_orient's body):
+// histogram, smoothing, peaks; writes out->ang[0..npk),
+// out->npk and *knpk_slot.  Returns npk (wave-uniform).
 template <int HS>
 __device__ __forceinline__ int orient_candidate(const Pyramid* __restrict__ py, const float* __restrict__ arena, CandOut* out,
-                                                uint32_t* knpk_slot, int img, uint32_t* hp, float* tf, float* hs, float* pang)
+                                                uint32_t* knpk_slot, int img, uint32_t* hp, float* tf, float* hs)
 {
     constexpr int NC = VO_ORIENT_COLS;
     const int lane = threadIdx.x;
@@ -1871,7 +1863,6 @@ __device__ __forceinline__ int orient_candidate(const Pyramid* __restrict__ py, 
     if (pk) {
         const int rank = __popcll(bal & ((1ull << lane) - 1ull));
         out->ang[rank] = ang;
-        if (pang) pang[rank] = ang;
     }
     __syncthreads();
     if (lane == 0) {
@@ -1906,7 +1897,7 @@ __global__ __launch_bounds__(64, VO_ORIENT_WAVES) void k_orient(const Pyramid* _
 #endif
         CandOut* out = cout + (size_t)img * cand_cap + kidx;
         if (!VO_ACC_LIST && __builtin_amdgcn_readfirstlane(out->npk) != -1) continue;
-        orient_candidate<HS>(py, arena, out, knpk + (size_t)img * cand_cap + kidx, img, hp, tf, hs, nullptr);
+        orient_candidate<HS>(py, arena, out, knpk + (size_t)img * cand_cap + kidx, img, hp, tf, hs);
     }
 }
 
@@ -1942,13 +1933,9 @@ __global__ __launch_bounds__(1024) void k_scan_cands(const CandOut* __restrict__
 
 // one thread per accepted candidate (k_refine's list; each writes its own keypoint slots, so the
 // list order does not matter)
-// With `sdesc` (k_orient_desc ran): the candidate's staged descriptors (CandOut.pad0 + p) move to
-// their keypoint rows (desc, meta) and no KpInt records are written.
 __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict__ n_acc, const int* __restrict__ acc,
                          const uint32_t* __restrict__ koff, vo_keypoint* __restrict__ kp, KpInt* __restrict__ kpi,
-                         int cand_cap, int kp_cap, int n_img, int upsample,
-                         const uint8_t* __restrict__ sdesc, const DescMeta* __restrict__ smeta,
-                         uint8_t* __restrict__ desc, DescMeta* __restrict__ meta)
+                         int cand_cap, int kp_cap, int n_img, int upsample)
 {
     __shared__ int fpre[VO_FLAT_MAX_IMG + 1];
     const long total = flat_setup(n_acc, cand_cap, n_img, fpre);
@@ -1976,28 +1963,10 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
             q.layer = co.layer;
             q.scale = co.scl * oscale;
             kp[(size_t)img * kp_cap + idx] = q;
-            if (sdesc) {
-                // the staged row (a permutation of the image's keypoints); past max_keypoints (the
-                // flagged overflow, VO_FLAG_KEYPOINTS) it was not computed: a zero descriptor
-                const uint32_t src = (uint32_t)co.pad0 + p;
-                typedef uint32_t u4c_t __attribute__((ext_vector_type(4)));
-                u4c_t* d4 = reinterpret_cast<u4c_t*>(desc + ((size_t)img * kp_cap + idx) * VO_DESC_LEN);
-                if (src < (uint32_t)kp_cap) {
-                    const u4c_t* s4 = reinterpret_cast<const u4c_t*>(sdesc + ((size_t)img * kp_cap + src) * VO_DESC_LEN);
-#pragma unroll
-                    for (int w = 0; w < VO_DESC_LEN / 16; ++w) d4[w] = s4[w];
-                    meta[(size_t)img * kp_cap + idx] = smeta[(size_t)img * kp_cap + src];
-                } else {
-#pragma unroll
-                    for (int w = 0; w < VO_DESC_LEN / 16; ++w) d4[w] = u4c_t{0u, 0u, 0u, 0u};
-                    meta[(size_t)img * kp_cap + idx] = DescMeta{0, 0.0f};
-                }
-            } else {
-                KpInt qi;
-                qi.xo = co.xo; qi.yo = co.yo; qi.scl = co.scl; qi.angle = co.ang[p];
-                qi.o = co.o; qi.layer = co.layer; qi.pad0 = 0; qi.pad1 = 0;
-                kpi[(size_t)img * kp_cap + idx] = qi;
-            }
+            KpInt qi;
+            qi.xo = co.xo; qi.yo = co.yo; qi.scl = co.scl; qi.angle = co.ang[p];
+            qi.o = co.o; qi.layer = co.layer; qi.pad0 = 0; qi.pad1 = 0;
+            kpi[(size_t)img * kp_cap + idx] = qi;
         }
     }
 }
@@ -2028,9 +1997,7 @@ __global__ void k_expand(const CandOut* __restrict__ cout, const int* __restrict
 #ifndef VO_DESC_U
 #define VO_DESC_U 2               // blocks of 64 samples per batch
 #endif
-#ifndef VO_ORIENT_DESC
-#define VO_ORIENT_DESC 1          // 0: k_orient, k_desc as separate passes (the window fetched twice)
-#endif
+
 // The keypoint's descriptor window tables into LDS (hdr, rtab, wtab; layout of dt_stride): its rotation,
 // radius, sample count, row table -- each window row i's column interval [jlo, jhi] inside the
 // rotated 4x4-cell square and the image interior, flattened by a prefix sum -- and the separable
@@ -2142,8 +2109,7 @@ __device__ __forceinline__ void desc_tables(const Pyramid* __restrict__ py, KpIn
     __syncthreads();
 }
 
-// The descriptor of one keypoint by the whole wave (k_desc's body; also the second half of
-// k_orient_desc): window tables, sample loop, histogram fold, normalisation, u8 quantisation;
+// The descriptor of one keypoint by the whole wave (k_desc's body): window tables, sample loop, histogram fold, normalisation, u8 quantisation;
 // writes dst[0..128) and *mdst.  hfx: DCOPIES * DCS words of LDS; dyn: dt_stride(dcap) words.
 template <int DCOPIES>
 __device__ __forceinline__ void desc_keypoint(const Pyramid* __restrict__ py, const float* __restrict__ arena, const KpInt q,
@@ -2353,63 +2319,6 @@ __global__ __launch_bounds__(64, VO_DESC_WAVES) void k_desc(const Pyramid* __res
         const KpInt q = kpi[(size_t)img * kp_cap + k];
         desc_keypoint<DCOPIES>(py, arena, q, img, dcap, hfx, dyn, desc + ((size_t)img * kp_cap + k) * VO_DESC_LEN,
                                meta + (size_t)img * kp_cap + k);
-    }
-}
-
-// Orientation and descriptors in one pass (VO.m:79-84): one wave per accepted candidate runs
-// orient_candidate, takes npk descriptor slots of its image (one atomic), and computes each
-// peak's descriptor (desc_keypoint) into the staging arrays.  The descriptor window of a
-// keypoint holds its orientation window (4.5 sigma < the rotated square's inscribed radius,
-// 7.5 sigma), so the descriptor's gradient loads find those lines in the cache the orientation
-// pass just filled: the window is fetched from HBM once instead of twice (k_orient then k_desc).
-// k_expand then writes the keypoints in candidate / peak order and moves each staged descriptor
-// to its keypoint's row.  The arithmetic of both halves is k_orient's and k_desc's, so every
-// bit is unchanged; slots past max_keypoints (the flagged overflow) are not computed.
-#ifndef VO_OD_WAVES
-#define VO_OD_WAVES 4             // k_orient_desc's register budget, waves per SIMD (5: 96 VGPRs, 40 spilled)
-#endif
-template <int HS, int DCOPIES>
-__global__ __launch_bounds__(64, VO_OD_WAVES) void k_orient_desc(const Pyramid* __restrict__ py, const float* __restrict__ arena,
-                                                    const int* __restrict__ n_acc, const int* __restrict__ acc,
-                                                    CandOut* __restrict__ cout, uint32_t* __restrict__ knpk,
-                                                    int* __restrict__ n_stage, uint8_t* __restrict__ sdesc,
-                                                    DescMeta* __restrict__ smeta, int cand_cap, int kp_cap, int n_img)
-{
-    constexpr int NC = VO_ORIENT_COLS;
-    static_assert(HS >= VO_SIFT_ORI_BINS && (HS * NC) % 4 == 0 && (NC == 64 || NC == 32 || NC == 16), "columns hold the 36 bins");
-    static_assert(DCS >= DHIST, "copy stride holds a histogram");
-    constexpr int HW = HS * NC > DCOPIES * DCS ? HS * NC : DCOPIES * DCS;
-    __shared__ __attribute__((aligned(16))) uint32_t hbuf[HW];      // orientation histogram, then descriptor copies
-    __shared__ float tf[VO_SIFT_ORI_BINS];
-    __shared__ float hs[VO_SIFT_ORI_BINS];
-    __shared__ float pang[VO_SIFT_MAX_PEAKS];
-    extern __shared__ uint32_t dyn[];                // descriptor tables (dt_stride(dcap)), then the image prefix
-    const int dcap = py->dcap, ts = dt_stride(dcap);
-    int* const fpre = reinterpret_cast<int*>(dyn + ts);
-    const int lane = threadIdx.x;
-    const long total = flat_setup(n_acc, cand_cap, n_img, fpre);
-    for (long t = blockIdx.x; t < total; t += gridDim.x) {
-        int img, a;
-        flat_find_wave(fpre, n_img, t, img, a);
-        const int kidx = __builtin_amdgcn_readfirstlane(acc[(size_t)img * cand_cap + a]);
-        CandOut* out = cout + (size_t)img * cand_cap + kidx;
-        const int npk = __builtin_amdgcn_readfirstlane(
-            orient_candidate<HS>(py, arena, out, knpk + (size_t)img * cand_cap + kidx, img, hbuf, tf, hs, pang));
-        int base = 0;
-        if (lane == 0 && npk > 0) {
-            base = atomicAdd(n_stage + img, npk);
-            out->pad0 = base;                            // k_expand reads the staged rows from here
-        }
-        base = __builtin_amdgcn_readfirstlane(base);
-        KpInt q;
-        q.xo = out->xo; q.yo = out->yo; q.scl = out->scl;
-        q.o = __builtin_amdgcn_readfirstlane(out->o); q.layer = __builtin_amdgcn_readfirstlane(out->layer);
-        q.pad0 = 0; q.pad1 = 0;
-        for (int p = 0; p < npk && base + p < kp_cap; ++p) {
-            q.angle = pang[p];
-            const size_t row = (size_t)img * kp_cap + base + p;
-            desc_keypoint<DCOPIES>(py, arena, q, img, dcap, hbuf, dyn, sdesc + row * VO_DESC_LEN, smeta + row);
-        }
     }
 }
 
@@ -2725,28 +2634,18 @@ void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const v
     float* A = b.arena;
     const dim3 gs(py.n_seg > 0 ? py.n_seg : 1, n_img);
     VO_LAUNCH(k_seg_count, gs, dim3(256), 0, s, b.mask, b.woff, py.n_words, py.n_seg);
-    VO_LAUNCH(k_seg_scan, dim3(n_img), dim3(1024), 0, s, b.woff, b.n_cand, b.n_acc, b.n_stage, py.n_seg);
+    VO_LAUNCH(k_seg_scan, dim3(n_img), dim3(1024), 0, s, b.woff, b.n_cand, b.n_acc, py.n_seg);
     VO_LAUNCH(k_seg_emit, gs, dim3(256), 0, s, d_py, b.mask, (const uint32_t*)b.woff, b.cand, b.cand_cap);
     VO_LAUNCH(k_refine, dim3(VO_REFINE_BLOCKS), dim3(256), 0, s, d_py, A, b.cand, b.n_cand, b.cout, b.acc, b.n_acc, b.koff, b.cand_cap, n_img,
               p.contrast_threshold, p.edge_threshold, p.sigma);
     const size_t fpre_bytes = sizeof(int) * (size_t)(n_img + 1);
     const int* n_walk = VO_ACC_LIST ? b.n_acc : b.n_cand;    // the accepted list, or every candidate
     const size_t dt_bytes = sizeof(uint32_t) * (size_t)dt_stride(py.dcap);
-    if (VO_ORIENT_DESC && VO_ACC_LIST) {
-        // orientation + descriptors in one pass, then the keypoint order
-        VO_LAUNCH_NAMED("k_orient_desc", (k_orient_desc<36, VO_DESC_COPIES>), dim3(kFeatureGrid), dim3(64),
-                        dt_bytes + fpre_bytes, s, d_py, A, n_walk, b.acc, b.cout, b.koff, b.n_stage, b.sdesc, b.smeta,
-                        b.cand_cap, b.kp_cap, n_img);
-        VO_LAUNCH(k_scan_cands, dim3(n_img), dim3(1024), 0, s, b.cout, b.n_cand, b.koff, b.n_kp, b.cand_cap);
-        VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, n_walk, b.acc, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
-                  n_img, p.upsample, b.sdesc, b.smeta, b.desc, b.meta);
-        return;
-    }
     VO_LAUNCH_NAMED("k_orient", (k_orient<36>), dim3(kFeatureGrid), dim3(64), fpre_bytes, s, d_py, A, n_walk, b.acc,
                     b.cout, b.koff, b.cand_cap, n_img);
     VO_LAUNCH(k_scan_cands, dim3(n_img), dim3(1024), 0, s, b.cout, b.n_cand, b.koff, b.n_kp, b.cand_cap);
     VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, n_walk, b.acc, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
-              n_img, p.upsample, (const uint8_t*)nullptr, (const DescMeta*)nullptr, (uint8_t*)nullptr, (DescMeta*)nullptr);
+              n_img, p.upsample);
     // 4 histogram copies: 2 -> +4 %, 8 -> +33 % k_desc time (MI355X)
     VO_LAUNCH_NAMED("k_desc", (k_desc<VO_DESC_COPIES>), dim3(kFeatureGrid), dim3(64), dt_bytes + fpre_bytes, s, d_py, A,
                     b.kpi, b.n_kp, b.desc, b.meta, b.kp_cap, n_img);

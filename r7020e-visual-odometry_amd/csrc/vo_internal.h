@@ -154,11 +154,6 @@ struct SiftBuffers {
     KpInt* kpi = nullptr;              // [n_img][kp_cap]
     uint8_t* desc = nullptr;           // [n_img][kp_cap][128]
     DescMeta* meta = nullptr;          // [n_img][kp_cap]
-    // k_orient_desc's descriptors in its own slot order (per image, slots taken by an atomic per
-    // candidate); k_expand moves them to keypoint order
-    int* n_stage = nullptr;            // [n_img]
-    uint8_t* sdesc = nullptr;          // [n_img][kp_cap][128]
-    DescMeta* smeta = nullptr;         // [n_img][kp_cap]
     int cand_cap = 0, kp_cap = 0, n_img = 0;
 };
 
