@@ -519,7 +519,11 @@ void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, con
                      compose ? &rest : nullptr);
         return;
     }
-    VO_LAUNCH(k_match_partial, dim3(2048), dim3(256), 0, s, d_jobs, n_jobs, b.partial, b.row_cap, b.n_chunks);
+#ifndef VO_TRACK_GRID
+#define VO_TRACK_GRID 2048        // k_match_partial workgroups for the tracking steps (the stereo matches: 2048)
+#endif
+    VO_LAUNCH(k_match_partial, dim3(compose ? VO_TRACK_GRID : 2048), dim3(256), 0, s, d_jobs, n_jobs, b.partial, b.row_cap,
+              b.n_chunks);
     if (VO_MATCH_FINISH) {
         MatchCompose cp{};
         if (compose) cp = *compose;
