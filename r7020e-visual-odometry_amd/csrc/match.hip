@@ -520,7 +520,9 @@ void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, con
         return;
     }
 #ifndef VO_TRACK_GRID
-#define VO_TRACK_GRID 2048        // k_match_partial workgroups for the tracking steps (the stereo matches: 2048)
+#define VO_TRACK_GRID 256         // k_match_partial workgroups for the tracking steps (stereo: 2048); 256 measured +1 % on the
+                                  // full path over 2048 (fewer resident beside the SIFT streams), 64 / 128 / 512 / 8192 not
+                                  // (profiles/r06_lm_ab_track_grid.txt)
 #endif
     VO_LAUNCH(k_match_partial, dim3(compose ? VO_TRACK_GRID : 2048), dim3(256), 0, s, d_jobs, n_jobs, b.partial, b.row_cap,
               b.n_chunks);
