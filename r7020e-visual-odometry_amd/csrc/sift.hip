@@ -1699,9 +1699,13 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
             scl = sigma * vo_expf(((float)layer + xi) / (float)L * 0.693147181f);
             resp = fabsf(contr);
         }
-        out->xo = xo; out->yo = yo; out->scl = scl; out->response = resp;
-        out->o = o; out->layer = layer; out->r = r; out->c = c;
-        out->npk = ok ? -1 : 0;
+        // a rejected candidate's record is read by nothing when the accepted list drives the
+        // later passes (k_orient / k_expand walk only the list; k_scan_cands reads knpk, VO_NPK_COMPACT)
+        if (ok || !VO_ACC_LIST || !VO_NPK_COMPACT) {
+            out->xo = xo; out->yo = yo; out->scl = scl; out->response = resp;
+            out->o = o; out->layer = layer; out->r = r; out->c = c;
+            out->npk = ok ? -1 : 0;
+        }
 #if VO_NPK_COMPACT
         knpk[(size_t)img * cand_cap + kidx] = ok ? 0xFFFFFFFFu : 0u;   // k_orient writes the accepted ones' count
 #endif
