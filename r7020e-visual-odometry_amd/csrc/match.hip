@@ -136,14 +136,8 @@ __device__ __forceinline__ v4i load_frag(const uint8_t* row, int off)
 #define MP_ROWS 128
 #define MP_LDS_ROW 144
 #define VO_MP_MAX_JOBS 256        // jobs per launch (one per thread of the task-table prologue)
-#ifndef VO_MATCH_BOUND
-#define VO_MATCH_BOUND 1          // integer pre-test of the top-2 epilogue (below); 0: every element converted
-#endif
 #ifndef VO_MP_BLOCKS
-// workgroups per CU the register budget is sized for: the pre-test's 16 bounds do not fit beside
-// the top-2 state in 168 VGPRs (28 spilled), 189 at 2 (2 and 3 measured equal without it,
-// profiles/r05_j_ab_match_diagnostics.txt)
-#define VO_MP_BLOCKS (VO_MATCH_BOUND ? 2 : 3)
+#define VO_MP_BLOCKS 3            // workgroups per CU the register budget is sized for
 #endif
 __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const MatchJob* __restrict__ jobs, int n_jobs,
                                                        MatchTop2* __restrict__ partial, int row_cap, int n_chunks_cap)
@@ -153,7 +147,6 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
     __shared__ __attribute__((aligned(16))) uint8_t bt[2][32 * MP_LDS_ROW];
     __shared__ int bck[2][32];
     __shared__ float binb[2][32];
-    __shared__ float smax[4];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l31 = lane & 31;
     const int lr = tid >> 3, lseg = tid & 7;              // loader: row lr of the tile, bytes [16 lseg, +16)
     // task table: job j owns tasks [tstart[j], tstart[j+1]); job sizes are read on device
@@ -221,30 +214,6 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
             rk[reg] = 128 * sa - 2097152;
             best[reg] = -INFINITY; second[reg] = -INFINITY; bidx[reg] = -1;
         }
-#if VO_MATCH_BOUND
-        // Integer pre-test of the epilogue.  The exact test is c > second with c = fl(fl(dot ina)
-        // inb); c is nondecreasing in inb, and inb <= inbmax (the chunk's largest 1/|b|), so
-        // dot <= D = floor(fl(second / fl(ina inbmax)) (1 - 2^-16)) implies c <= second: the
-        // roundings move c by at most (1 + 2^-24)^6, far inside the 2^-16 margin (second > 0;
-        // second <= 0 gives D <= 0 and ina = 0 or inbmax = 0 a D of +2^30, both conservative).
-        // So an element with dot <= D can never update its row, and the wave converts a pair
-        // of rows to float only when some lane's dot exceeds its D -- the same updates as the
-        // plain epilogue, bit for bit.  D is refreshed only when second changes.
-        float inbmax = 0.0f;
-        for (int jc = j0 + tid; jc < j1; jc += 256) {
-            const int rb = J.idx2 ? gld(J.idx2 + jc) : jc;
-            inbmax = fmaxf(inbmax, gld_meta(J.m2 + rb).inv_norm);
-        }
-        inbmax = half_max(inbmax);
-        inbmax = fmaxf(inbmax, __shfl_xor(inbmax, 32));
-        if (lane == 0) smax[wave] = inbmax;
-        auto bound = [&](int q) {
-            const float d = (second[q] / (ina[q] * inbmax)) * 0.99998474f;
-            const float f = floorf(d);
-            return !(f > -1073741824.0f) ? -1073741824 : (f > 1073741824.0f ? 1073741824 : (int)f);
-        };
-        int dq[16];
-#endif
         // loader: column jt + lr (clamped into the chunk; the epilogue masks columns >= j1)
         v4i gv;
         DescMeta gm;
@@ -269,11 +238,6 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
         };
         gload(j0);
         __syncthreads();                                   // previous task's readers are done with bt
-#if VO_MATCH_BOUND
-        inbmax = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) dq[reg] = bound(reg);
-#endif
         lstore(0);
         if (j0 + 32 < j1) gload(j0 + 32);
         int buf = 0;
@@ -304,13 +268,9 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
 #else
 #pragma unroll
             for (int reg = 0; reg < 16; reg += 2) {
-                const int d0 = accv[reg] + rk[reg] + ck, d1 = accv[reg + 1] + rk[reg + 1] + ck;   // exact dots
-#if VO_MATCH_BOUND
-                if (!__builtin_amdgcn_ballot_w64(d0 > dq[reg] || d1 > dq[reg + 1])) continue;   // wave-uniform
-#endif
                 // c for two accumulator rows at once: the two products as packed f32 muls
                 // (each component an IEEE multiply, same bits as the scalar form)
-                const vo_f2 fp = vo_f2{(float)d0, (float)d1};
+                const vo_f2 fp = vo_f2{(float)(accv[reg] + rk[reg] + ck), (float)(accv[reg + 1] + rk[reg + 1] + ck)};
                 vo_f2 cp = (fp * vo_f2{ina[reg], ina[reg + 1]}) * vo_f2{inb, inb};
                 cp = cp + vo_f2{cmask, cmask};
 #pragma unroll
@@ -322,9 +282,6 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
                         second[q] = g1 ? best[q] : (g2 ? c : second[q]);
                         best[q] = g1 ? c : best[q];
                         bidx[q] = g1 ? jc : bidx[q];
-#if VO_MATCH_BOUND
-                        dq[q] = bound(q);
-#endif
                     }
                 }
             }
@@ -333,10 +290,6 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
             if ((tno & (tno - 1)) == 0) {                  // wave-uniform
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) second[reg] = half_max(second[reg]);
-#if VO_MATCH_BOUND
-#pragma unroll
-                for (int reg = 0; reg < 16; ++reg) dq[reg] = bound(reg);
-#endif
             }
         }
         // merge the 32 lanes of each half (same accumulator rows, different columns)
