@@ -151,7 +151,11 @@ def sequence_leg(args, torch, rank, world, local, dist, barrier, max_over_ranks,
     render_s = time.perf_counter() - t0
     rp = vo.default_ransac_params()
     rp.max_num_trials = 2048                                   # BASELINE configs[2]
-    SB = args.seq_batch
+    # frames per submit: --seq-batch, but at least 8 submits per rank's block so the three-deep
+    # pipeline's fill and drain stay a small part of it (8 ranks over KITTI-00: 568-frame blocks,
+    # 71 per submit; one rank: 256)
+    block = -(-n // world)
+    SB = max(1, min(args.seq_batch, max(16, -(-block // 8))))
     ctx = vo.Context(street.KITTI_ROWS, street.KITTI_COLS, SB, device=local, calib=vo.calib_from(P0, P1), ransac=rp)
     seq = (dL, dR, P0, P1)
     ctx.reset()                                                # warm-up: the block's first two batches
