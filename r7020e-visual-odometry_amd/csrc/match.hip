@@ -139,6 +139,12 @@ __device__ __forceinline__ v4i load_frag(const uint8_t* row, int off)
 #ifndef VO_MP_BLOCKS
 #define VO_MP_BLOCKS 3            // workgroups per CU the register budget is sized for
 #endif
+#ifndef VO_MP_BSEARCH
+// 1: binary search of a task's job in the task table (8 dependent LDS reads); 0: the linear scan
+// (up to 255).  k_match_partial 0.623 against 0.667 / 0.679 ms isolated per 256-frame step
+// (profiles/r06_r_ab_match_task.txt)
+#define VO_MP_BSEARCH 1
+#endif
 __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const MatchJob* __restrict__ jobs, int n_jobs,
                                                        MatchTop2* __restrict__ partial, int row_cap, int n_chunks_cap)
 {
@@ -173,9 +179,17 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
         __syncthreads();
     }
     const int total = tstart[n_jobs];
+    // (an XCD-contiguous task order -- one job's row blocks, which read the same F2 tiles, on one
+    // XCD's L2 -- measured slower: 0.825 against 0.667 ms isolated, profiles/r06_r_ab_match_task.txt)
     for (int t = blockIdx.x; t < total; t += gridDim.x) {       // workgroup-uniform
         int jb = 0;
+#if VO_MP_BSEARCH
+        // last job whose first task <= t (tstart is nondecreasing; empty jobs repeat a value)
+        for (int step = VO_MP_MAX_JOBS / 2; step >= 1; step >>= 1)
+            if (jb + step < n_jobs && tstart[jb + step] <= t) jb += step;
+#else
         while (jb + 1 < n_jobs && tstart[jb + 1] <= t) ++jb;
+#endif
         const int n1 = jn1[jb], nch = jnch[jb];
         const int n2 = job_rows(jobs[jb].n2, row_cap);
         const long rel = t - tstart[jb];
