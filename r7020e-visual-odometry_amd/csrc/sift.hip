@@ -1699,13 +1699,14 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
             scl = sigma * vo_expf(((float)layer + xi) / (float)L * 0.693147181f);
             resp = fabsf(contr);
         }
-        // a rejected candidate's record is read by nothing when the accepted list drives the
-        // later passes (k_orient / k_expand walk only the list; k_scan_cands reads knpk, VO_NPK_COMPACT)
-        if (ok || !VO_ACC_LIST || !VO_NPK_COMPACT) {
-            out->xo = xo; out->yo = yo; out->scl = scl; out->response = resp;
-            out->o = o; out->layer = layer; out->r = r; out->c = c;
-            out->npk = ok ? -1 : 0;
-        }
+        // Every candidate's record is stored, although with the accepted list (VO_ACC_LIST,
+        // VO_NPK_COMPACT) nothing reads a rejected one's: storing only the accepted ones (~13 %)
+        // cut k_refine's own time 1.14 -> 0.98 ms and its PMC bytes 5.34 -> 4.84 GB per 256-frame
+        // step, but the step got 3 % slower (10181 -> 9878 stereo frames/s on one box, the level
+        // blurs beside it 20.4 -> 21.6 ms in situ, profiles/r06_s_ab_round6_bisect.txt)
+        out->xo = xo; out->yo = yo; out->scl = scl; out->response = resp;
+        out->o = o; out->layer = layer; out->r = r; out->c = c;
+        out->npk = ok ? -1 : 0;
 #if VO_NPK_COMPACT
         knpk[(size_t)img * cand_cap + kidx] = ok ? 0xFFFFFFFFu : 0u;   // k_orient writes the accepted ones' count
 #endif
@@ -2651,7 +2652,10 @@ void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const v
     VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, n_walk, b.acc, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
               n_img, p.upsample);
     // 4 histogram copies: 2 -> +4 %, 8 -> +33 % k_desc time (MI355X)
-    VO_LAUNCH_NAMED("k_desc", (k_desc<VO_DESC_COPIES>), dim3(kFeatureGrid), dim3(64), dt_bytes + fpre_bytes, s, d_py, A,
+#ifndef VO_DESC_LDS_PAD
+#define VO_DESC_LDS_PAD 0         // extra dynamic LDS per k_desc workgroup (bytes): caps its residency per CU
+#endif
+    VO_LAUNCH_NAMED("k_desc", (k_desc<VO_DESC_COPIES>), dim3(kFeatureGrid), dim3(64), dt_bytes + fpre_bytes + VO_DESC_LDS_PAD, s, d_py, A,
                     b.kpi, b.n_kp, b.desc, b.meta, b.kp_cap, n_img);
 }
 
