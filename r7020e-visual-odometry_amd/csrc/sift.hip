@@ -2652,10 +2652,10 @@ void sift_enqueue_features(const Pyramid& py, SiftBuffers& b, int n_img, const v
     VO_LAUNCH(k_expand, dim3(256), dim3(256), 0, s, b.cout, n_walk, b.acc, b.koff, b.kp, b.kpi, b.cand_cap, b.kp_cap,
               n_img, p.upsample);
     // 4 histogram copies: 2 -> +4 %, 8 -> +33 % k_desc time (MI355X)
-#ifndef VO_DESC_LDS_PAD
-#define VO_DESC_LDS_PAD 0         // extra dynamic LDS per k_desc workgroup (bytes): caps its residency per CU
-#endif
-    VO_LAUNCH_NAMED("k_desc", (k_desc<VO_DESC_COPIES>), dim3(kFeatureGrid), dim3(64), dt_bytes + fpre_bytes + VO_DESC_LDS_PAD, s, d_py, A,
+    // (capping k_desc's residency per CU with 8 / 16 / 28 KB of extra LDS per workgroup, to leave
+    // the level blurs beside it more waves: 8886 / 8016 / 6877 against 10186 stereo frames/s --
+    // the blurs gain 3 ms in situ, k_desc loses 3-11 ms, profiles/r06_t_ab_desc_lds_pad.txt)
+    VO_LAUNCH_NAMED("k_desc", (k_desc<VO_DESC_COPIES>), dim3(kFeatureGrid), dim3(64), dt_bytes + fpre_bytes, s, d_py, A,
                     b.kpi, b.n_kp, b.desc, b.meta, b.kp_cap, n_img);
 }
 
