@@ -1703,15 +1703,11 @@ __global__ __launch_bounds__(256) void k_refine(const Pyramid* __restrict__ py, 
         // VO_NPK_COMPACT) nothing reads a rejected one's: storing only the accepted ones (~13 %)
         // cut k_refine's own time 1.14 -> 0.98 ms and its PMC bytes 5.34 -> 4.84 GB per 256-frame
         // step, but the step got 3 % slower (10181 -> 9878 stereo frames/s on one box, the level
-        // blurs beside it 20.4 -> 21.6 ms in situ, profiles/r06_s_ab_round6_bisect.txt)
-#ifndef VO_REFINE_ACC_ONLY
-#define VO_REFINE_ACC_ONLY 0
-#endif
-        if (ok || !VO_REFINE_ACC_ONLY || !VO_ACC_LIST || !VO_NPK_COMPACT) {
-            out->xo = xo; out->yo = yo; out->scl = scl; out->response = resp;
-            out->o = o; out->layer = layer; out->r = r; out->c = c;
-            out->npk = ok ? -1 : 0;
-        }
+        // blurs beside it 20.4 -> 21.6 ms in situ, profiles/r06_s_ab_round6_bisect.txt; re-measured
+        // with the full path: configs[1] -2.4 %, full path within noise, r06_v_ab_fullpath_cpl_refine.txt)
+        out->xo = xo; out->yo = yo; out->scl = scl; out->response = resp;
+        out->o = o; out->layer = layer; out->r = r; out->c = c;
+        out->npk = ok ? -1 : 0;
 #if VO_NPK_COMPACT
         knpk[(size_t)img * cand_cap + kidx] = ok ? 0xFFFFFFFFu : 0u;   // k_orient writes the accepted ones' count
 #endif
@@ -2382,10 +2378,10 @@ static bool launch_blur_r(dim3 grid, hipStream_t s, const float* src, size_t pla
 #endif
         constexpr int kMaxTH = VO_BLUR_MAX_TH, kWaveTarget = VO_BLUR_WAVES, kCpl2MaxC = VO_CPL2_MAXC;
         const bool base = name[7] == 'b';
-#ifndef VO_CPL2_MINR
-#define VO_CPL2_MINR 99           // level blurs of at least this radius use 2 columns per lane on every plane
-#endif
-        const int cpl = (!base && (C <= kCpl2MaxC || RAD >= VO_CPL2_MINR)) ? 2 : 4;
+        // (2 columns per lane for the octave-0 levels of radius >= 13 / 10 / 8 too -- fewer registers,
+        // so more of them fit beside the tracking matches of the full path: configs[1] -0.8 / -0.9 /
+        // -4.3 %, full path within noise, profiles/r06_v_ab_fullpath_cpl_refine.txt)
+        const int cpl = (!base && C <= kCpl2MaxC) ? 2 : 4;
         const int n_strips = (C + 64 * cpl - 1) / (64 * cpl);
         const long rows_total = (long)R * n_strips * grid.z;
         // (the staged octave-0 base stages at most kBaseMaxTH-row bands: its LDS is sized for them)
