@@ -21,6 +21,7 @@ namespace vo {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 typedef float vo_f2 __attribute__((ext_vector_type(2)));
+typedef float vo_f4 __attribute__((ext_vector_type(4)));
 
 // Ranking in the cosine domain.  The spec's SSD is sv = 2 - 2c with
 // c = ((float)dot * inv|a|) * inv|b|; sv is a non-increasing function of c, so the
@@ -139,6 +140,12 @@ __device__ __forceinline__ v4i load_frag(const uint8_t* row, int off)
 #ifndef VO_MP_BLOCKS
 #define VO_MP_BLOCKS 3            // workgroups per CU the register budget is sized for
 #endif
+#ifndef VO_MATCH_T
+#define VO_MATCH_T 1              // 1: transposed tile (F2 x F1): one F1 row per lane, a per-tile max pre-test
+#endif
+#ifndef VO_MATCH_T_RAISE
+#define VO_MATCH_T_RAISE 0
+#endif
 #ifndef VO_MP_BSEARCH
 // 1: binary search of a task's job in the task table (8 dependent LDS reads); 0: the linear scan
 // (up to 255).  k_match_partial 0.623 against 0.667 / 0.679 ms isolated per 256-frame step
@@ -151,8 +158,8 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
     // F2 tile rows padded to 144 B (36 dwords): the 32 lanes of a half read 16 B at row l31,
     // so a 128-B stride would put them all on the same banks
     __shared__ __attribute__((aligned(16))) uint8_t bt[2][32 * MP_LDS_ROW];
-    __shared__ int bck[2][32];
-    __shared__ float binb[2][32];
+    __shared__ __attribute__((aligned(16))) int bck[2][32];
+    __shared__ __attribute__((aligned(16))) float binb[2][32];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l31 = lane & 31;
     const int lr = tid >> 3, lseg = tid & 7;              // loader: row lr of the tile, bytes [16 lseg, +16)
     // task table: job j owns tasks [tstart[j], tstart[j+1]); job sizes are read on device
@@ -211,6 +218,25 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
                 for (int kk = 0; kk < 4; ++kk) a[kk] = (v4i){0, 0, 0, 0};
             }
         }
+#if VO_MATCH_T
+        // transposed form: the lane's one F1 row (i0 + l31; both halves hold it) and its running
+        // top-2 over the F2 columns this lane sees
+        int rk1 = 0;
+        float ina1 = 0.0f;
+        {
+            const int ia = i0 + l31;
+            if (ia < n1) {
+                const int ra = J.idx1 ? gld(J.idx1 + ia) : ia;
+                const DescMeta m = gld_meta(J.m1 + ra);
+                rk1 = 128 * m.sum - 2097152;
+                ina1 = m.inv_norm;
+            } else {
+                rk1 = -2097152;
+            }
+        }
+        float best1 = -INFINITY, second1 = -INFINITY;
+        int bidx1 = -1;
+#else
         int rk[16];
         float ina[16];
         float best[16], second[16];
@@ -228,6 +254,7 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
             rk[reg] = 128 * sa - 2097152;
             best[reg] = -INFINITY; second[reg] = -INFINITY; bidx[reg] = -1;
         }
+#endif
         // loader: column jt + lr (clamped into the chunk; the epilogue masks columns >= j1)
         v4i gv;
         DescMeta gm;
@@ -267,6 +294,59 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
             const uint8_t* brow = &bt[buf][l31 * MP_LDS_ROW + 16 * h];
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) b[kk] = *reinterpret_cast<const v4i*>(brow + 32 * kk);
+#if VO_MATCH_T
+            // D = F2 tile (A operand, from LDS) x F1 rows (B operand, registers): lane l holds F1
+            // row i0 + l31 and F2 columns jt + (reg & 3) + 8 (reg >> 2) + 4 h, reg = 0..15 --
+            // ascending in reg, so the lane meets its columns in ascending order
+            v16i accv = (v16i){0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) accv = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[kk], a[kk], accv, 0, 0, 0);
+            float cv[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                // the column metadata of regs 4q .. 4q+3: tile columns 8q + 4h .. +3 (one broadcast
+                // 16-B read each)
+                const v4i ck4 = *reinterpret_cast<const v4i*>(&bck[buf][8 * q + 4 * h]);
+                const vo_f4 ib4 = *reinterpret_cast<const vo_f4*>(&binb[buf][8 * q + 4 * h]);
+#pragma unroll
+                for (int i = 0; i < 4; i += 2) {
+                    // c = ((float)dot * inv|a|) * inv|b|, two columns at once as packed f32 muls
+                    const vo_f2 fp = vo_f2{(float)(accv[4 * q + i] + rk1 + ck4[i]), (float)(accv[4 * q + i + 1] + rk1 + ck4[i + 1])};
+                    const vo_f2 cp = (fp * vo_f2{ina1, ina1}) * vo_f2{ib4[i], ib4[i + 1]};
+                    cv[4 * q + i] = cp.x;
+                    cv[4 * q + i + 1] = cp.y;
+                }
+            }
+            if (jt + 32 > j1) {                            // wave-uniform: the ragged last tile
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg)
+                    cv[reg] = jt + (reg & 3) + 8 * (reg >> 2) + 4 * h < j1 ? cv[reg] : -INFINITY;
+            }
+            // exact pre-test: a tile whose 16 values are all <= the lane's second best changes
+            // nothing (the update below leaves best / second / index as they are for c <= second)
+            float m = fmaxf(fmaxf(fmaxf(cv[0], cv[1]), fmaxf(cv[2], cv[3])), fmaxf(fmaxf(cv[4], cv[5]), fmaxf(cv[6], cv[7])));
+            m = fmaxf(m, fmaxf(fmaxf(fmaxf(cv[8], cv[9]), fmaxf(cv[10], cv[11])), fmaxf(fmaxf(cv[12], cv[13]), fmaxf(cv[14], cv[15]))));
+            if (__builtin_amdgcn_ballot_w64(m > second1)) {
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg) {
+                    const float c = cv[reg];
+                    const bool g1 = c > best1, g2 = c > second1;
+                    second1 = g1 ? best1 : (g2 ? c : second1);
+                    best1 = g1 ? c : best1;
+                    bidx1 = g1 ? jt + (reg & 3) + 8 * (reg >> 2) + 4 * h : bidx1;
+                }
+            }
+#if VO_MATCH_T_RAISE
+            // after tiles 1, 2, 4, 8, ... of the chunk both halves' second best of the row is raised to
+            // the larger of the two (the row's second best so far is at least that): every later
+            // column has a larger index than every column either half has seen, so a value <= the
+            // raised second can never enter the row's final top-2 (it only loses ties)
+            ++tno;
+            if ((tno & (tno - 1)) == 0) second1 = fmaxf(second1, __shfl_xor(second1, 32));
+#else
+            (void)tno;
+#endif
+#else
             const int ck = bck[buf][l31];
             const float inb = binb[buf][l31];
             v16i accv = (v16i){0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -305,7 +385,22 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) second[reg] = half_max(second[reg]);
             }
+#endif
         }
+#if VO_MATCH_T
+        // the two halves hold the same F1 row (different F2 columns): merge, half 0 writes
+        {
+            const float ob = __shfl_xor(best1, 32), os = __shfl_xor(second1, 32);
+            const int oi = __shfl_xor(bidx1, 32);
+            top2c_merge(best1, bidx1, second1, ob, oi, os);
+            const int row = i0 + l31;
+            if (h == 0 && row < n1) {
+                MatchTop2 mt;
+                mt.best = best1; mt.idx = bidx1; mt.second = second1; mt.pad = 0;
+                partial[((size_t)jb * n_chunks_cap + chunk) * row_cap + row] = mt;
+            }
+        }
+#else
         // merge the 32 lanes of each half (same accumulator rows, different columns)
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) half_top2c(best[reg], bidx[reg], second[reg]);
@@ -323,6 +418,7 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
                 partial[((size_t)jb * n_chunks_cap + chunk) * row_cap + row] = m;
             }
         }
+#endif
     }
 }
 
@@ -538,7 +634,10 @@ void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, con
                                   // full path over 2048 (fewer resident beside the SIFT streams), 64 / 128 / 512 / 8192 not
                                   // (profiles/r06_lm_ab_track_grid.txt)
 #endif
-    VO_LAUNCH(k_match_partial, dim3(compose ? VO_TRACK_GRID : 2048), dim3(256), 0, s, d_jobs, n_jobs, b.partial, b.row_cap,
+#ifndef VO_STEREO_GRID
+#define VO_STEREO_GRID 2048
+#endif
+    VO_LAUNCH(k_match_partial, dim3(compose ? VO_TRACK_GRID : VO_STEREO_GRID), dim3(256), 0, s, d_jobs, n_jobs, b.partial, b.row_cap,
               b.n_chunks);
     if (VO_MATCH_FINISH) {
         MatchCompose cp{};
