@@ -7,12 +7,12 @@
 // v_mfma_i32_32x32x32_i8 on (a - 128) x (b - 128), corrected by the row sums
 //   dot(a,b) = dot(a',b') + 128 (sum a + sum b) - 2^21,
 // so the result is exact and order-free; MFMA throughput is 8x the v_dot4
-// VALU path.  The top-2 search is fused into the MFMA epilogue: each lane keeps
-// (best, idx, second) for its 16 accumulator rows, halves merge by DPP rotations
-// and a permlane swap with a (value, index) total order, chunks of F2 merge in
-// k_match_merge (one thread per F1 row), which also applies MatchThreshold /
-// MaxRatio; k_match_compact writes the pairs in ascending F1 order with a block
-// prefix sum.
+// VALU path.  The top-2 search is fused into the MFMA epilogue: the tile is computed
+// transposed (F2 columns x F1 rows), so each lane keeps (best, idx, second) for ONE F1
+// row over the F2 columns it holds, the two half-waves that share a row merge with a
+// (value, index) total order, and the F2 chunks merge in k_match_finish (one workgroup
+// per job), which also applies MatchThreshold / MaxRatio and writes the pairs in
+// ascending F1 order (k_match_merge + k_match_compact with VO_MATCH_FINISH=0).
 #include "vo_internal.h"
 #include "vo_geom.h"
 
@@ -38,52 +38,6 @@ __device__ __forceinline__ void top2c_merge(float& b, int& i, float& s, float b2
     const float ns = fmaxf(fmaxf(s, s2), fminf(b, b2));
     if (b2 > b || (b2 == b && i2 < i)) { b = b2; i = i2; }
     s = ns;
-}
-
-// Cross-lane steps within a 32-lane half without LDS: DPP row rotations (every lane of a
-// 16-lane row receives a valid source) and v_permlane16_swap for the other row of the half.
-// The merges they feed (max, top2c_merge) are associative and commutative, so rotations
-// give every lane the same result as the xor butterfly.
-template <int CTRL>
-__device__ __forceinline__ int dpp_i(int v)
-{
-    return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, false);
-}
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v)
-{
-    return __int_as_float(dpp_i<CTRL>(__float_as_int(v)));
-}
-__device__ __forceinline__ int xor16_i(int v)               // the value of lane l ^ 16
-{
-    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    return (threadIdx.x & 16) ? p[0] : p[1];
-}
-__device__ __forceinline__ float xor16_f(float v)
-{
-    return __int_as_float(xor16_i(__float_as_int(v)));
-}
-enum : int { VO_DPP_ROR1 = 0x121, VO_DPP_ROR2 = 0x122, VO_DPP_ROR4 = 0x124, VO_DPP_ROR8 = 0x128 };
-__device__ __forceinline__ float half_max(float m)           // max over the lane's 32-lane half
-{
-    m = fmaxf(m, dpp_f<VO_DPP_ROR8>(m));
-    m = fmaxf(m, dpp_f<VO_DPP_ROR4>(m));
-    m = fmaxf(m, dpp_f<VO_DPP_ROR2>(m));
-    m = fmaxf(m, dpp_f<VO_DPP_ROR1>(m));
-    return fmaxf(m, xor16_f(m));
-}
-template <int CTRL>
-__device__ __forceinline__ void top2c_step(float& b, int& i, float& s)
-{
-    top2c_merge(b, i, s, dpp_f<CTRL>(b), dpp_i<CTRL>(i), dpp_f<CTRL>(s));
-}
-__device__ __forceinline__ void half_top2c(float& b, int& i, float& s)   // merge over the 32-lane half
-{
-    top2c_step<VO_DPP_ROR8>(b, i, s);
-    top2c_step<VO_DPP_ROR4>(b, i, s);
-    top2c_step<VO_DPP_ROR2>(b, i, s);
-    top2c_step<VO_DPP_ROR1>(b, i, s);
-    top2c_merge(b, i, s, xor16_f(b), xor16_i(i), xor16_f(s));
 }
 
 // Pointers read from the job table are generic to the compiler, so loads through them became
@@ -128,23 +82,21 @@ __device__ __forceinline__ v4i load_frag(const uint8_t* row, int off)
 // One workgroup (4 waves) per (job, 128-row F1 block, CHUNK-column F2 chunk); wave w owns
 // F1 rows [128 blk + 32 w, +32).  The F2 side is shared: each 32-column tile (4 KB of
 // descriptors + metadata) is loaded once per workgroup, one 16-B load per thread, staged
-// through a double-buffered LDS tile, and read by every wave as MFMA B fragments.  Tile t+1
-// is written to LDS and tile t+2 is in flight from HBM/L2 while tile t runs its 4 MFMAs
-// and epilogue.  Epilogue per accumulator element: dot = acc + 128 sa - 2^21 + 128 sb (one
-// add3), c = ((float)dot * inv|a|) * inv|b| (packed muls, two rows at once), then the top-2
-// update, skipped by the wave when no lane's c beats its row's second best.  The half-wave
-// reductions (second-best refresh, final merge) use DPP rotations and v_permlane16_swap.
+// through a double-buffered LDS tile, and read by every wave as the MFMA A operand (the
+// wave's F1 rows are the B operand, in registers): D = F2 tile x F1 rows, so lane l holds F1
+// row l & 31 and 16 of the tile's columns.  Tile t+1 is written to LDS and tile t+2 is in
+// flight from HBM/L2 while tile t runs its 4 MFMAs and epilogue.  Epilogue per accumulator
+// element: dot = acc + 128 sa - 2^21 + 128 sb (one add3), c = ((float)dot * inv|a|) * inv|b|
+// (packed muls, two columns at once); then one exact pre-test per tile -- the max of the
+// lane's 16 values against its second best -- before the in-order top-2 update, which the wave
+// skips when no lane passes.  (The untransposed tile -- D = F1 x F2, 16 rows' top-2 state per
+// lane, 154 VGPRs, one wave vote per element -- measured 23 % slower isolated and cost the full
+// path 3 %: its 3 waves per SIMD held register file the level blurs needed, r06_w.)
 #define MP_ROWS 128
 #define MP_LDS_ROW 144
 #define VO_MP_MAX_JOBS 256        // jobs per launch (one per thread of the task-table prologue)
 #ifndef VO_MP_BLOCKS
 #define VO_MP_BLOCKS 3            // workgroups per CU the register budget is sized for
-#endif
-#ifndef VO_MATCH_T
-#define VO_MATCH_T 1              // 1: transposed tile (F2 x F1): one F1 row per lane, a per-tile max pre-test
-#endif
-#ifndef VO_MATCH_T_RAISE
-#define VO_MATCH_T_RAISE 0
 #endif
 #ifndef VO_MP_BSEARCH
 // 1: binary search of a task's job in the task table (8 dependent LDS reads); 0: the linear scan
@@ -218,7 +170,6 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
                 for (int kk = 0; kk < 4; ++kk) a[kk] = (v4i){0, 0, 0, 0};
             }
         }
-#if VO_MATCH_T
         // transposed form: the lane's one F1 row (i0 + l31; both halves hold it) and its running
         // top-2 over the F2 columns this lane sees
         int rk1 = 0;
@@ -236,25 +187,6 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
         }
         float best1 = -INFINITY, second1 = -INFINITY;
         int bidx1 = -1;
-#else
-        int rk[16];
-        float ina[16];
-        float best[16], second[16];
-        int bidx[16];
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            const int row = i0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-            int sa = 0;
-            ina[reg] = 0.0f;
-            if (row < n1) {
-                const int ra = J.idx1 ? gld(J.idx1 + row) : row;
-                const DescMeta m = gld_meta(J.m1 + ra);
-                sa = m.sum; ina[reg] = m.inv_norm;
-            }
-            rk[reg] = 128 * sa - 2097152;
-            best[reg] = -INFINITY; second[reg] = -INFINITY; bidx[reg] = -1;
-        }
-#endif
         // loader: column jt + lr (clamped into the chunk; the epilogue masks columns >= j1)
         v4i gv;
         DescMeta gm;
@@ -264,14 +196,6 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
             gv = gld(reinterpret_cast<const v4i*>(J.d2 + (size_t)rb * VO_DESC_LEN + 16 * lseg));
             if (lseg == 0) gm = gld_meta(J.m2 + rb);
         };
-        // After tiles 1, 2, 4, 8, ... of the chunk every lane's second best of a row is raised
-        // to the max over the 32 lanes of the half (the row's wave-wide second best so far).
-        // The merged top-2 is unchanged: each lane's second is a candidate value other than
-        // its own best, so every second (raised or not) is <= the row's true second, which
-        // the merge still finds.  A value <= the raised second can never enter the row's final
-        // top-2 (later columns only lose ties), so the wave skips the update unless some lane
-        // beats its second -- rare once the row has settled.
-        int tno = 0;
         auto lstore = [&](int buf) {                       // stored as b - 128 (the MFMA operand)
             *reinterpret_cast<v4i*>(&bt[buf][lr * MP_LDS_ROW + 16 * lseg]) =
                 gv ^ (v4i){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
@@ -286,15 +210,12 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
             __syncthreads();                               // tile jt visible; tile jt-32's buffer free
             if (jt + 32 < j1) {
                 lstore(buf ^ 1);                           // tile jt+32 (loaded one iteration ago)
-#if !(defined(VO_MATCH_DIAG) && VO_MATCH_DIAG == 2)
-                if (jt + 64 < j1) gload(jt + 64);          // (diagnostic build 2: no F2 loads after the first)
-#endif
+                if (jt + 64 < j1) gload(jt + 64);
             }
             v4i b[4];
             const uint8_t* brow = &bt[buf][l31 * MP_LDS_ROW + 16 * h];
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) b[kk] = *reinterpret_cast<const v4i*>(brow + 32 * kk);
-#if VO_MATCH_T
             // D = F2 tile (A operand, from LDS) x F1 rows (B operand, registers): lane l holds F1
             // row i0 + l31 and F2 columns jt + (reg & 3) + 8 (reg >> 2) + 4 h, reg = 0..15 --
             // ascending in reg, so the lane meets its columns in ascending order
@@ -336,58 +257,7 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
                     bidx1 = g1 ? jt + (reg & 3) + 8 * (reg >> 2) + 4 * h : bidx1;
                 }
             }
-#if VO_MATCH_T_RAISE
-            // after tiles 1, 2, 4, 8, ... of the chunk both halves' second best of the row is raised to
-            // the larger of the two (the row's second best so far is at least that): every later
-            // column has a larger index than every column either half has seen, so a value <= the
-            // raised second can never enter the row's final top-2 (it only loses ties)
-            ++tno;
-            if ((tno & (tno - 1)) == 0) second1 = fmaxf(second1, __shfl_xor(second1, 32));
-#else
-            (void)tno;
-#endif
-#else
-            const int ck = bck[buf][l31];
-            const float inb = binb[buf][l31];
-            v16i accv = (v16i){0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) accv = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kk], b[kk], accv, 0, 0, 0);
-            const int jc = jt + l31;
-            // ragged last tile: masked columns get c = -inf (never ranked); elsewhere c + 0 = c
-            // exactly (c >= +0)
-            const float cmask = jc < j1 ? 0.0f : -INFINITY;
-#if defined(VO_MATCH_DIAG) && VO_MATCH_DIAG == 1
-            // diagnostic build 1 (timing only): no epilogue, the accumulators feed one running max
-            for (int reg = 0; reg < 16; ++reg) best[reg] = fmaxf(best[reg], (float)accv[reg] + cmask);
-#else
-#pragma unroll
-            for (int reg = 0; reg < 16; reg += 2) {
-                // c for two accumulator rows at once: the two products as packed f32 muls
-                // (each component an IEEE multiply, same bits as the scalar form)
-                const vo_f2 fp = vo_f2{(float)(accv[reg] + rk[reg] + ck), (float)(accv[reg + 1] + rk[reg + 1] + ck)};
-                vo_f2 cp = (fp * vo_f2{ina[reg], ina[reg + 1]}) * vo_f2{inb, inb};
-                cp = cp + vo_f2{cmask, cmask};
-#pragma unroll
-                for (int h2 = 0; h2 < 2; ++h2) {
-                    const int q = reg + h2;
-                    const float c = h2 ? cp.y : cp.x;
-                    if (__builtin_amdgcn_ballot_w64(c > second[q])) {
-                        const bool g1 = c > best[q], g2 = c > second[q];
-                        second[q] = g1 ? best[q] : (g2 ? c : second[q]);
-                        best[q] = g1 ? c : best[q];
-                        bidx[q] = g1 ? jc : bidx[q];
-                    }
-                }
-            }
-#endif
-            ++tno;
-            if ((tno & (tno - 1)) == 0) {                  // wave-uniform
-#pragma unroll
-                for (int reg = 0; reg < 16; ++reg) second[reg] = half_max(second[reg]);
-            }
-#endif
         }
-#if VO_MATCH_T
         // the two halves hold the same F1 row (different F2 columns): merge, half 0 writes
         {
             const float ob = __shfl_xor(best1, 32), os = __shfl_xor(second1, 32);
@@ -400,25 +270,6 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
                 partial[((size_t)jb * n_chunks_cap + chunk) * row_cap + row] = mt;
             }
         }
-#else
-        // merge the 32 lanes of each half (same accumulator rows, different columns)
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) half_top2c(best[reg], bidx[reg], second[reg]);
-        if (l31 < 16) {
-            // lane l31 of half h writes accumulator row `l31` (select by unrolled compare)
-            float bb = -INFINITY, ss = -INFINITY;
-            int ii = -1;
-#pragma unroll
-            for (int reg = 0; reg < 16; ++reg)
-                if (reg == l31) { bb = best[reg]; ii = bidx[reg]; ss = second[reg]; }
-            const int row = i0 + (l31 & 3) + 8 * (l31 >> 2) + 4 * h;
-            if (row < n1) {
-                MatchTop2 m;
-                m.best = bb; m.idx = ii; m.second = ss; m.pad = 0;
-                partial[((size_t)jb * n_chunks_cap + chunk) * row_cap + row] = m;
-            }
-        }
-#endif
     }
 }
 
