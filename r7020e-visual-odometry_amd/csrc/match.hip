@@ -96,7 +96,7 @@ __device__ __forceinline__ v4i load_frag(const uint8_t* row, int off)
 #define MP_LDS_ROW 144
 #define VO_MP_MAX_JOBS 256        // jobs per launch (one per thread of the task-table prologue)
 #ifndef VO_MP_BLOCKS
-#define VO_MP_BLOCKS 3            // workgroups per CU the register budget is sized for
+#define VO_MP_BLOCKS 5            // workgroups per CU the register budget of k_match_partial<1> is sized for (92 VGPRs)
 #endif
 #ifndef VO_MP_BSEARCH
 // 1: binary search of a task's job in the task table (8 dependent LDS reads); 0: the linear scan
@@ -104,9 +104,13 @@ __device__ __forceinline__ v4i load_frag(const uint8_t* row, int off)
 // (profiles/r06_r_ab_match_task.txt)
 #define VO_MP_BSEARCH 1
 #endif
-__global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const MatchJob* __restrict__ jobs, int n_jobs,
+// NB: 32-row F1 sub-blocks per wave (MP_ROWS * NB rows per workgroup); NB = 2 runs two
+// independent MFMA chains per tile on the same F2 fragments (half the LDS reads per MFMA)
+template <int NB>
+__global__ __launch_bounds__(256, NB == 1 ? VO_MP_BLOCKS : 2) void k_match_partial(const MatchJob* __restrict__ jobs, int n_jobs,
                                                        MatchTop2* __restrict__ partial, int row_cap, int n_chunks_cap)
 {
+    constexpr int ROWS = MP_ROWS * NB;
     // F2 tile rows padded to 144 B (36 dwords): the 32 lanes of a half read 16 B at row l31,
     // so a 128-B stride would put them all on the same banks
     __shared__ __attribute__((aligned(16))) uint8_t bt[2][32 * MP_LDS_ROW];
@@ -124,7 +128,7 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
             const int n1 = job_rows(jobs[tid].n1, row_cap), n2 = job_rows(jobs[tid].n2, row_cap);
             const int nch = (n2 + VO_MATCH_CHUNK - 1) / VO_MATCH_CHUNK;
             jn1[tid] = n1; jnch[tid] = nch;
-            my = ((n1 + MP_ROWS - 1) / MP_ROWS) * nch;
+            my = ((n1 + ROWS - 1) / ROWS) * nch;
         }
         int inc = my;
 #pragma unroll
@@ -154,39 +158,34 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
         const long rel = t - tstart[jb];
         const MatchJob J = jobs[jb];
         const int blk = (int)(rel / nch), chunk = (int)(rel - (long)blk * nch);
-        const int i0 = blk * MP_ROWS + 32 * wave, j0 = chunk * VO_MATCH_CHUNK;
+        const int i0 = blk * ROWS + 32 * NB * wave, j0 = chunk * VO_MATCH_CHUNK;
         const int j1 = min(j0 + VO_MATCH_CHUNK, n2);
-        // A fragments: F1 row i0 + l31, bytes [32kk + 16h, +16)
-        v4i a[4];
-        {
-            const int ia = i0 + l31;
+        // F1 fragments (the MFMA B operand) of sub-block sb: row i0 + 32 sb + l31, bytes
+        // [32kk + 16h, +16); the lane's row's sum term and inverse norm; its running top-2 over
+        // the F2 columns this lane sees (both halves hold the row)
+        v4i a[NB][4];
+        int rk1[NB];
+        float ina1[NB], best1[NB], second1[NB];
+        int bidx1[NB];
+#pragma unroll
+        for (int sb = 0; sb < NB; ++sb) {
+            const int ia = i0 + 32 * sb + l31;
+            rk1[sb] = -2097152;
+            ina1[sb] = 0.0f;
             if (ia < n1) {
                 const int ra = J.idx1 ? gld(J.idx1 + ia) : ia;
                 const uint8_t* row = J.d1 + (size_t)ra * VO_DESC_LEN;
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) a[kk] = load_frag(row, 32 * kk + 16 * h);
+                for (int kk = 0; kk < 4; ++kk) a[sb][kk] = load_frag(row, 32 * kk + 16 * h);
+                const DescMeta m = gld_meta(J.m1 + ra);
+                rk1[sb] = 128 * m.sum - 2097152;
+                ina1[sb] = m.inv_norm;
             } else {
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) a[kk] = (v4i){0, 0, 0, 0};
+                for (int kk = 0; kk < 4; ++kk) a[sb][kk] = (v4i){0, 0, 0, 0};
             }
+            best1[sb] = -INFINITY; second1[sb] = -INFINITY; bidx1[sb] = -1;
         }
-        // transposed form: the lane's one F1 row (i0 + l31; both halves hold it) and its running
-        // top-2 over the F2 columns this lane sees
-        int rk1 = 0;
-        float ina1 = 0.0f;
-        {
-            const int ia = i0 + l31;
-            if (ia < n1) {
-                const int ra = J.idx1 ? gld(J.idx1 + ia) : ia;
-                const DescMeta m = gld_meta(J.m1 + ra);
-                rk1 = 128 * m.sum - 2097152;
-                ina1 = m.inv_norm;
-            } else {
-                rk1 = -2097152;
-            }
-        }
-        float best1 = -INFINITY, second1 = -INFINITY;
-        int bidx1 = -1;
         // loader: column jt + lr (clamped into the chunk; the epilogue masks columns >= j1)
         v4i gv;
         DescMeta gm;
@@ -219,9 +218,15 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
             // D = F2 tile (A operand, from LDS) x F1 rows (B operand, registers): lane l holds F1
             // row i0 + l31 and F2 columns jt + (reg & 3) + 8 (reg >> 2) + 4 h, reg = 0..15 --
             // ascending in reg, so the lane meets its columns in ascending order
-            v16i accv = (v16i){0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+            v16i accv[NB];
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) accv = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[kk], a[kk], accv, 0, 0, 0);
+            for (int sb = 0; sb < NB; ++sb) accv[sb] = (v16i){0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int sb = 0; sb < NB; ++sb) accv[sb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[kk], a[sb][kk], accv[sb], 0, 0, 0);
+#pragma unroll
+            for (int sb = 0; sb < NB; ++sb) {
             float cv[16];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -232,8 +237,9 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
 #pragma unroll
                 for (int i = 0; i < 4; i += 2) {
                     // c = ((float)dot * inv|a|) * inv|b|, two columns at once as packed f32 muls
-                    const vo_f2 fp = vo_f2{(float)(accv[4 * q + i] + rk1 + ck4[i]), (float)(accv[4 * q + i + 1] + rk1 + ck4[i + 1])};
-                    const vo_f2 cp = (fp * vo_f2{ina1, ina1}) * vo_f2{ib4[i], ib4[i + 1]};
+                    const vo_f2 fp = vo_f2{(float)(accv[sb][4 * q + i] + rk1[sb] + ck4[i]),
+                                           (float)(accv[sb][4 * q + i + 1] + rk1[sb] + ck4[i + 1])};
+                    const vo_f2 cp = (fp * vo_f2{ina1[sb], ina1[sb]}) * vo_f2{ib4[i], ib4[i + 1]};
                     cv[4 * q + i] = cp.x;
                     cv[4 * q + i + 1] = cp.y;
                 }
@@ -247,26 +253,28 @@ __global__ __launch_bounds__(256, VO_MP_BLOCKS) void k_match_partial(const Match
             // nothing (the update below leaves best / second / index as they are for c <= second)
             float m = fmaxf(fmaxf(fmaxf(cv[0], cv[1]), fmaxf(cv[2], cv[3])), fmaxf(fmaxf(cv[4], cv[5]), fmaxf(cv[6], cv[7])));
             m = fmaxf(m, fmaxf(fmaxf(fmaxf(cv[8], cv[9]), fmaxf(cv[10], cv[11])), fmaxf(fmaxf(cv[12], cv[13]), fmaxf(cv[14], cv[15]))));
-            if (__builtin_amdgcn_ballot_w64(m > second1)) {
+            if (__builtin_amdgcn_ballot_w64(m > second1[sb])) {
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) {
                     const float c = cv[reg];
-                    const bool g1 = c > best1, g2 = c > second1;
-                    second1 = g1 ? best1 : (g2 ? c : second1);
-                    best1 = g1 ? c : best1;
-                    bidx1 = g1 ? jt + (reg & 3) + 8 * (reg >> 2) + 4 * h : bidx1;
+                    const bool g1 = c > best1[sb], g2 = c > second1[sb];
+                    second1[sb] = g1 ? best1[sb] : (g2 ? c : second1[sb]);
+                    best1[sb] = g1 ? c : best1[sb];
+                    bidx1[sb] = g1 ? jt + (reg & 3) + 8 * (reg >> 2) + 4 * h : bidx1[sb];
                 }
+            }
             }
         }
         // the two halves hold the same F1 row (different F2 columns): merge, half 0 writes
-        {
-            const float ob = __shfl_xor(best1, 32), os = __shfl_xor(second1, 32);
-            const int oi = __shfl_xor(bidx1, 32);
-            top2c_merge(best1, bidx1, second1, ob, oi, os);
-            const int row = i0 + l31;
+#pragma unroll
+        for (int sb = 0; sb < NB; ++sb) {
+            const float ob = __shfl_xor(best1[sb], 32), os = __shfl_xor(second1[sb], 32);
+            const int oi = __shfl_xor(bidx1[sb], 32);
+            top2c_merge(best1[sb], bidx1[sb], second1[sb], ob, oi, os);
+            const int row = i0 + 32 * sb + l31;
             if (h == 0 && row < n1) {
                 MatchTop2 mt;
-                mt.best = best1; mt.idx = bidx1; mt.second = second1; mt.pad = 0;
+                mt.best = best1[sb]; mt.idx = bidx1[sb]; mt.second = second1[sb]; mt.pad = 0;
                 partial[((size_t)jb * n_chunks_cap + chunk) * row_cap + row] = mt;
             }
         }
@@ -488,8 +496,10 @@ void match_launch(const MatchBuffers& b, const MatchJob* d_jobs, int n_jobs, con
 #ifndef VO_STEREO_GRID
 #define VO_STEREO_GRID 2048
 #endif
-    VO_LAUNCH(k_match_partial, dim3(compose ? VO_TRACK_GRID : VO_STEREO_GRID), dim3(256), 0, s, d_jobs, n_jobs, b.partial, b.row_cap,
-              b.n_chunks);
+    // (two F1 sub-blocks per wave for the stereo matches, k_match_partial<2> at 165 VGPRs: configs[1]
+    // -1 %, the 1080p block 0.123 against 0.128 of i8 peak, profiles/r06_y_ab_match_nb2_chunk.txt)
+    VO_LAUNCH_NAMED("k_match_partial", k_match_partial<1>, dim3(compose ? VO_TRACK_GRID : VO_STEREO_GRID), dim3(256), 0, s,
+                    d_jobs, n_jobs, b.partial, b.row_cap, b.n_chunks);
     if (VO_MATCH_FINISH) {
         MatchCompose cp{};
         if (compose) cp = *compose;

@@ -117,7 +117,7 @@ MAX_PEAKS = 18            # VO_SIFT_MAX_PEAKS
 CANDOUT_BYTES = 48 + 4 * (MAX_PEAKS + 2)
 KP_BYTES = 32             # vo_keypoint; the internal KpInt record is 32 B too
 DESC_BYTES = 128 + 8      # u8 descriptor + DescMeta
-MATCH_CHUNK = 2048        # VO_MATCH_CHUNK
+MATCH_CHUNK = 4096        # VO_MATCH_CHUNK
 ORI_RADIUS, DESCR_SCL, DESCR_WIDTH = 4.5, 3.0, 4
 
 

@@ -42,9 +42,10 @@ def test_sift_match_assorted_sizes(vo, oracle, syn, rows, cols, k):
 @pytest.mark.parametrize("seed", range(6))
 def test_match_ties_bit_exact(vo, oracle, seed):
     """Rows whose best and second-best candidates are exact duplicates, permuted copies or
-    one-unit perturbations (equal or adjacent SSD), spread over several 2048-column chunks."""
+    one-unit perturbations (equal or adjacent SSD), spread over two F2 chunks (VO_MATCH_CHUNK =
+    4096 columns), so the chunk merge of k_match_finish sees the ties too."""
     rng = np.random.default_rng(100 + seed)
-    n1, n2 = 300 + 37 * seed, 2500 + 211 * seed
+    n1, n2 = 300 + 37 * seed, 4500 + 211 * seed
     F1 = rng.integers(0, 90, (n1, 128)).astype(np.uint8)
     F2 = rng.integers(0, 90, (n2, 128)).astype(np.uint8)
     for i in range(n1):
