@@ -98,6 +98,7 @@ __device__ __forceinline__ v4i load_frag(const uint8_t* row, int off)
 #ifndef VO_MP_BLOCKS
 #define VO_MP_BLOCKS 5            // workgroups per CU the register budget of k_match_partial<1> is sized for (92 VGPRs)
 #endif
+#define MP_NBUF 2
 #ifndef VO_MP_BSEARCH
 // 1: binary search of a task's job in the task table (8 dependent LDS reads); 0: the linear scan
 // (up to 255).  k_match_partial 0.623 against 0.667 / 0.679 ms isolated per 256-frame step
@@ -113,9 +114,9 @@ __global__ __launch_bounds__(256, NB == 1 ? VO_MP_BLOCKS : 2) void k_match_parti
     constexpr int ROWS = MP_ROWS * NB;
     // F2 tile rows padded to 144 B (36 dwords): the 32 lanes of a half read 16 B at row l31,
     // so a 128-B stride would put them all on the same banks
-    __shared__ __attribute__((aligned(16))) uint8_t bt[2][32 * MP_LDS_ROW];
-    __shared__ __attribute__((aligned(16))) int bck[2][32];
-    __shared__ __attribute__((aligned(16))) float binb[2][32];
+    __shared__ __attribute__((aligned(16))) uint8_t bt[MP_NBUF][32 * MP_LDS_ROW];
+    __shared__ __attribute__((aligned(16))) int bck[MP_NBUF][32];
+    __shared__ __attribute__((aligned(16))) float binb[MP_NBUF][32];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l31 = lane & 31;
     const int lr = tid >> 3, lseg = tid & 7;              // loader: row lr of the tile, bytes [16 lseg, +16)
     // task table: job j owns tasks [tstart[j], tstart[j+1]); job sizes are read on device
@@ -200,6 +201,65 @@ __global__ __launch_bounds__(256, NB == 1 ? VO_MP_BLOCKS : 2) void k_match_parti
                 gv ^ (v4i){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
             if (lseg == 0) { bck[buf][lr] = 128 * gm.sum; binb[buf][lr] = gm.inv_norm; }
         };
+        // the tile's MFMAs: D = F2 tile (A operand, from LDS) x F1 rows (B operand, registers):
+        // lane l holds F1 row i0 + 32 sb + l31 and F2 columns jt + (reg & 3) + 8 (reg >> 2) + 4 h,
+        // reg = 0..15 -- ascending in reg, so the lane meets its columns in ascending order
+        auto tile_mfma = [&](int bi, v16i (&accv)[NB]) {
+            v4i b[4];
+            const uint8_t* brow = &bt[bi][l31 * MP_LDS_ROW + 16 * h];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) b[kk] = *reinterpret_cast<const v4i*>(brow + 32 * kk);
+#pragma unroll
+            for (int sb = 0; sb < NB; ++sb) accv[sb] = (v16i){0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int sb = 0; sb < NB; ++sb) accv[sb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[kk], a[sb][kk], accv[sb], 0, 0, 0);
+        };
+        auto tile_epilogue = [&](int bi, int jt, const v16i (&accv)[NB]) {
+#pragma unroll
+            for (int sb = 0; sb < NB; ++sb) {
+                float cv[16];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    // the column metadata of regs 4q .. 4q+3: tile columns 8q + 4h .. +3 (one
+                    // broadcast 16-B read each)
+                    const v4i ck4 = *reinterpret_cast<const v4i*>(&bck[bi][8 * q + 4 * h]);
+                    const vo_f4 ib4 = *reinterpret_cast<const vo_f4*>(&binb[bi][8 * q + 4 * h]);
+#pragma unroll
+                    for (int i = 0; i < 4; i += 2) {
+                        // c = ((float)dot * inv|a|) * inv|b|, two columns at once as packed f32 muls
+                        const vo_f2 fp = vo_f2{(float)(accv[sb][4 * q + i] + rk1[sb] + ck4[i]),
+                                               (float)(accv[sb][4 * q + i + 1] + rk1[sb] + ck4[i + 1])};
+                        const vo_f2 cp = (fp * vo_f2{ina1[sb], ina1[sb]}) * vo_f2{ib4[i], ib4[i + 1]};
+                        cv[4 * q + i] = cp.x;
+                        cv[4 * q + i + 1] = cp.y;
+                    }
+                }
+                if (jt + 32 > j1) {                        // wave-uniform: the ragged last tile
+#pragma unroll
+                    for (int reg = 0; reg < 16; ++reg)
+                        cv[reg] = jt + (reg & 3) + 8 * (reg >> 2) + 4 * h < j1 ? cv[reg] : -INFINITY;
+                }
+                // exact pre-test: a tile whose 16 values are all <= the lane's second best changes
+                // nothing (the update below leaves best / second / index as they are for c <= second)
+                float m = fmaxf(fmaxf(fmaxf(cv[0], cv[1]), fmaxf(cv[2], cv[3])), fmaxf(fmaxf(cv[4], cv[5]), fmaxf(cv[6], cv[7])));
+                m = fmaxf(m, fmaxf(fmaxf(fmaxf(cv[8], cv[9]), fmaxf(cv[10], cv[11])), fmaxf(fmaxf(cv[12], cv[13]), fmaxf(cv[14], cv[15]))));
+                if (__builtin_amdgcn_ballot_w64(m > second1[sb])) {
+#pragma unroll
+                    for (int reg = 0; reg < 16; ++reg) {
+                        const float c = cv[reg];
+                        const bool g1 = c > best1[sb], g2 = c > second1[sb];
+                        second1[sb] = g1 ? best1[sb] : (g2 ? c : second1[sb]);
+                        best1[sb] = g1 ? c : best1[sb];
+                        bidx1[sb] = g1 ? jt + (reg & 3) + 8 * (reg >> 2) + 4 * h : bidx1[sb];
+                    }
+                }
+            }
+        };
+        // (a three-tile pipeline -- tile t+1's MFMAs issued before tile t's epilogue, 116 VGPRs at 4
+        // waves per SIMD -- measured slower: 0.453 against 0.420 ms isolated, the 1080p block 0.121
+        // against 0.129 of i8 peak, profiles/r06_za_ab_match_pipe_grid.txt)
         gload(j0);
         __syncthreads();                                   // previous task's readers are done with bt
         lstore(0);
@@ -211,61 +271,10 @@ __global__ __launch_bounds__(256, NB == 1 ? VO_MP_BLOCKS : 2) void k_match_parti
                 lstore(buf ^ 1);                           // tile jt+32 (loaded one iteration ago)
                 if (jt + 64 < j1) gload(jt + 64);
             }
-            v4i b[4];
-            const uint8_t* brow = &bt[buf][l31 * MP_LDS_ROW + 16 * h];
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) b[kk] = *reinterpret_cast<const v4i*>(brow + 32 * kk);
-            // D = F2 tile (A operand, from LDS) x F1 rows (B operand, registers): lane l holds F1
-            // row i0 + l31 and F2 columns jt + (reg & 3) + 8 (reg >> 2) + 4 h, reg = 0..15 --
-            // ascending in reg, so the lane meets its columns in ascending order
             v16i accv[NB];
-#pragma unroll
-            for (int sb = 0; sb < NB; ++sb) accv[sb] = (v16i){0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-                for (int sb = 0; sb < NB; ++sb) accv[sb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(b[kk], a[sb][kk], accv[sb], 0, 0, 0);
-#pragma unroll
-            for (int sb = 0; sb < NB; ++sb) {
-            float cv[16];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                // the column metadata of regs 4q .. 4q+3: tile columns 8q + 4h .. +3 (one broadcast
-                // 16-B read each)
-                const v4i ck4 = *reinterpret_cast<const v4i*>(&bck[buf][8 * q + 4 * h]);
-                const vo_f4 ib4 = *reinterpret_cast<const vo_f4*>(&binb[buf][8 * q + 4 * h]);
-#pragma unroll
-                for (int i = 0; i < 4; i += 2) {
-                    // c = ((float)dot * inv|a|) * inv|b|, two columns at once as packed f32 muls
-                    const vo_f2 fp = vo_f2{(float)(accv[sb][4 * q + i] + rk1[sb] + ck4[i]),
-                                           (float)(accv[sb][4 * q + i + 1] + rk1[sb] + ck4[i + 1])};
-                    const vo_f2 cp = (fp * vo_f2{ina1[sb], ina1[sb]}) * vo_f2{ib4[i], ib4[i + 1]};
-                    cv[4 * q + i] = cp.x;
-                    cv[4 * q + i + 1] = cp.y;
-                }
-            }
-            if (jt + 32 > j1) {                            // wave-uniform: the ragged last tile
-#pragma unroll
-                for (int reg = 0; reg < 16; ++reg)
-                    cv[reg] = jt + (reg & 3) + 8 * (reg >> 2) + 4 * h < j1 ? cv[reg] : -INFINITY;
-            }
-            // exact pre-test: a tile whose 16 values are all <= the lane's second best changes
-            // nothing (the update below leaves best / second / index as they are for c <= second)
-            float m = fmaxf(fmaxf(fmaxf(cv[0], cv[1]), fmaxf(cv[2], cv[3])), fmaxf(fmaxf(cv[4], cv[5]), fmaxf(cv[6], cv[7])));
-            m = fmaxf(m, fmaxf(fmaxf(fmaxf(cv[8], cv[9]), fmaxf(cv[10], cv[11])), fmaxf(fmaxf(cv[12], cv[13]), fmaxf(cv[14], cv[15]))));
-            if (__builtin_amdgcn_ballot_w64(m > second1[sb])) {
-#pragma unroll
-                for (int reg = 0; reg < 16; ++reg) {
-                    const float c = cv[reg];
-                    const bool g1 = c > best1[sb], g2 = c > second1[sb];
-                    second1[sb] = g1 ? best1[sb] : (g2 ? c : second1[sb]);
-                    best1[sb] = g1 ? c : best1[sb];
-                    bidx1[sb] = g1 ? jt + (reg & 3) + 8 * (reg >> 2) + 4 * h : bidx1[sb];
-                }
-            }
-            }
+            tile_mfma(buf, accv);
+            tile_epilogue(buf, jt, accv);
         }
-        // the two halves hold the same F1 row (different F2 columns): merge, half 0 writes
 #pragma unroll
         for (int sb = 0; sb < NB; ++sb) {
             const float ob = __shfl_xor(best1[sb], 32), os = __shfl_xor(second1[sb], 32);
