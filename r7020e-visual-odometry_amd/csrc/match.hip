@@ -242,7 +242,11 @@ __global__ __launch_bounds__(256, NB == 1 ? VO_MP_BLOCKS : 2) void k_match_parti
                         cv[reg] = jt + (reg & 3) + 8 * (reg >> 2) + 4 * h < j1 ? cv[reg] : -INFINITY;
                 }
                 // exact pre-test: a tile whose 16 values are all <= the lane's second best changes
-                // nothing (the update below leaves best / second / index as they are for c <= second)
+                // nothing (the update below leaves best / second / index as they are for c <= second).
+                // (An integer pre-test before the float conversion -- the tile's dots against
+                // floor(second / inv|a| / max inv|b| (1 - 2^-16)) -- was bit-exact but 27 % slower:
+                // the bound with the tile's largest inv|b| rarely clears a whole wave, so it only
+                // added work, profiles/r06_zd_ab_match_ibound.txt)
                 float m = fmaxf(fmaxf(fmaxf(cv[0], cv[1]), fmaxf(cv[2], cv[3])), fmaxf(fmaxf(cv[4], cv[5]), fmaxf(cv[6], cv[7])));
                 m = fmaxf(m, fmaxf(fmaxf(fmaxf(cv[8], cv[9]), fmaxf(cv[10], cv[11])), fmaxf(fmaxf(cv[12], cv[13]), fmaxf(cv[14], cv[15]))));
                 if (__builtin_amdgcn_ballot_w64(m > second1[sb])) {
